@@ -33,13 +33,17 @@ def pyramid_level_shapes(h, w, levels):
 
 
 def corr_volume(fmap1, fmap2):
-    """(B,C,H,W) x2 -> (B, H*W, H, W): raft.py:26-33."""
-    b, c, h, w = fmap1.shape
-    f1 = fmap1.reshape(b, c, h * w)
+    """(B,C,H,W) x2 -> (B, H*W, H, W): raft.py:26-33.
+
+    fmap1 may hold any subset of query pixels (B,C,h1,w1); targets always follow fmap2's grid.
+    """
+    b, c, h1, w1 = fmap1.shape
+    h, w = fmap2.shape[-2:]
+    f1 = fmap1.reshape(b, c, h1 * w1)
     f2 = fmap2.reshape(b, c, h * w)
     corr = np.matmul(f1.transpose(0, 2, 1), f2)
     corr = corr / np.sqrt(np.asarray(c, dtype=fmap1.dtype))
-    return corr.reshape(b, h * w, h, w)
+    return corr.reshape(b, h1 * w1, h, w)
 
 
 def _avg_pool2(x):

@@ -1,0 +1,74 @@
+// capi.cpp — host-side parts of the C ABI: error state, version, pyramid geometry.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "rmd.h"
+
+namespace rmd {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+void clear_error() { g_err[0] = '\0'; }
+
+static int level_tile(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
+
+}  // namespace rmd
+
+extern "C" const char* rmd_last_error(void) { return rmd::g_err; }
+
+extern "C" const char* rmd_version(void) { return "rmd 0.1 gfx950"; }
+
+extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels, int storage,
+                                    rmd_pyramid_desc* d) {
+    if (!d) {
+        rmd::set_error("rmd_pyramid_describe: null desc");
+        return RMD_ERR_ARG;
+    }
+    if (storage != RMD_F32 && storage != RMD_F16) {
+        rmd::set_error("rmd_pyramid_describe: storage must be RMD_F32 or RMD_F16");
+        return RMD_ERR_ARG;
+    }
+    if (batch < 1 || height < 1 || width < 1 || levels < 1 || levels > RMD_MAX_LEVELS) {
+        rmd::set_error("rmd_pyramid_describe: bad sizes (batch=%d height=%d width=%d levels=%d)", batch, height,
+                       width, levels);
+        return RMD_ERR_SHAPE;
+    }
+    std::memset(d, 0, sizeof(*d));
+    d->batch = batch;
+    d->height = height;
+    d->width = width;
+    d->levels = levels;
+    d->storage = storage;
+    const long long n = (long long)height * width;
+    long long off = 0;
+    int h = height, w = width;
+    for (int l = 0; l < levels; ++l) {
+        if (h < 1 || w < 1) {
+            // avg_pool2d of a 1-pixel map fails in the reference as well ("output size is too small")
+            rmd::set_error("rmd_pyramid_describe: level %d of a %dx%d map is empty", l, height, width);
+            return RMD_ERR_SHAPE;
+        }
+        const int t = rmd::level_tile(l);
+        d->level_h[l] = h;
+        d->level_w[l] = w;
+        d->tile_h[l] = t;
+        d->tile_w[l] = t;
+        d->tiles_y[l] = (h + t - 1) / t;
+        d->tiles_x[l] = (w + t - 1) / t;
+        d->level_offset[l] = off;
+        off += (long long)batch * d->tiles_y[l] * d->tiles_x[l] * n * t * t;
+        h /= 2;
+        w /= 2;
+    }
+    d->total_elements = off;
+    rmd::clear_error();
+    return RMD_OK;
+}

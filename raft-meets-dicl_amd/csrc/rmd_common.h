@@ -1,0 +1,73 @@
+// rmd_common.h — shared host/device helpers for the gfx950 cost-volume kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "rmd.h"
+
+namespace rmd {
+
+// ---- error reporting (C-ABI: negative code + per-thread message) -------------------------------
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define RMD_REQUIRE(cond, code, ...)        \
+    do {                                    \
+        if (!(cond)) {                      \
+            ::rmd::set_error(__VA_ARGS__);  \
+            return (code);                  \
+        }                                   \
+    } while (0)
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+        return RMD_ERR_LAUNCH;
+    }
+    clear_error();
+    return RMD_OK;
+}
+
+// ---- pyramid geometry (POD copy of rmd_pyramid_desc, passed by value to kernels) --------------
+struct PyrGeom {
+    int batch, height, width, levels;
+    int lh[RMD_MAX_LEVELS], lw[RMD_MAX_LEVELS];
+    int th[RMD_MAX_LEVELS], tw[RMD_MAX_LEVELS];
+    int ty[RMD_MAX_LEVELS], tx[RMD_MAX_LEVELS];
+    long long off[RMD_MAX_LEVELS];
+};
+
+inline PyrGeom make_geom(const rmd_pyramid_desc& d) {
+    PyrGeom g{};
+    g.batch = d.batch;
+    g.height = d.height;
+    g.width = d.width;
+    g.levels = d.levels;
+    for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
+        g.lh[l] = d.level_h[l];
+        g.lw[l] = d.level_w[l];
+        g.th[l] = d.tile_h[l];
+        g.tw[l] = d.tile_w[l];
+        g.ty[l] = d.tiles_y[l];
+        g.tx[l] = d.tiles_x[l];
+        g.off[l] = d.level_offset[l];
+    }
+    return g;
+}
+
+// tile edge of level l: 8, 8, 4, 2 — a 16x16 level-0 target block maps to whole tiles on
+// every level
+__host__ __device__ constexpr int level_tile(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
+
+}  // namespace rmd

@@ -1,0 +1,88 @@
+"""ctypes binding of librmd.so — the C ABI declared in include/rmd.h.
+
+This is the reference-side binding a maintainer of qzed/raft-meets-dicl would add:
+plain pointers, sizes and the current HIP stream.  There is no CPU fallback: if the library is
+missing, or a tensor is not on the GPU, the call raises.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's libamdhip64 first so librmd.so binds to the same HIP runtime)
+
+RMD_OK = 0
+RMD_F32, RMD_F16, RMD_BF16 = 0, 1, 2
+MAX_LEVELS = 4
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RMD_LIBRARY", os.path.join(_HERE, "librmd.so"))
+
+
+class PyramidDesc(ctypes.Structure):
+    """Mirror of rmd_pyramid_desc (include/rmd.h)."""
+
+    _fields_ = [
+        ("batch", ctypes.c_int), ("height", ctypes.c_int), ("width", ctypes.c_int),
+        ("levels", ctypes.c_int), ("storage", ctypes.c_int),
+        ("level_h", ctypes.c_int * MAX_LEVELS), ("level_w", ctypes.c_int * MAX_LEVELS),
+        ("tile_h", ctypes.c_int * MAX_LEVELS), ("tile_w", ctypes.c_int * MAX_LEVELS),
+        ("tiles_y", ctypes.c_int * MAX_LEVELS), ("tiles_x", ctypes.c_int * MAX_LEVELS),
+        ("level_offset", ctypes.c_longlong * MAX_LEVELS),
+        ("total_elements", ctypes.c_longlong),
+    ]
+
+
+class RmdError(RuntimeError):
+    pass
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_U = ctypes.c_uint
+_SIGS = {
+    "rmd_pyramid_describe": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(PyramidDesc)]),
+    "rmd_corr_pyramid_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PyramidDesc), _I, _I]),
+    "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
+    "rmd_corr_lookup": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
+    "rmd_last_error": (ctypes.c_char_p, []),
+    "rmd_version": (ctypes.c_char_p, []),
+}
+
+
+def lib():
+    """Load librmd.so once; raise loudly if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RmdError(f"rmd: HIP library not found at {LIB_PATH}; build it with "
+                           f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def symbols():
+    return sorted(_SIGS)
+
+
+def check(rc, what):
+    if rc != RMD_OK:
+        msg = lib().rmd_last_error().decode(errors="replace")
+        raise RmdError(f"{what} failed (code {rc}): {msg}")
+
+
+def describe(batch, height, width, levels, storage):
+    d = PyramidDesc()
+    check(lib().rmd_pyramid_describe(batch, height, width, levels, storage, ctypes.byref(d)),
+          "rmd_pyramid_describe")
+    return d
+
+
+def stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
