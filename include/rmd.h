@@ -42,17 +42,19 @@ extern "C" {
 
 /*
  * Layout of a correlation pyramid in HBM (one allocation, `total_elements` elements of
- * `storage` type).  Level l has floor-halved sizes level_h[l] x level_w[l] (raft.py:38-47) and is
- * cut into tile_h[l] x tile_w[l] target tiles (8x8, 8x8, 4x4, 2x2).  Tiles are query-minor:
+ * `storage` type).  Level l has floor-halved sizes level_h[l] x level_w[l] (raft.py:38-47).  Each
+ * target row is cut into chunks of tile_w[l] = 8, 8, 4, 2 elements (tile_h[l] = 1) and chunks are
+ * QUERY-MINOR:
  *
  *   element(b, p, y, x) at level l =
  *     level_offset[l] + ((((b*tiles_y[l] + y/tile_h[l])*tiles_x[l] + x/tile_w[l]) * (H*W) + p)
  *                        * tile_h[l]*tile_w[l]) + (y%tile_h[l])*tile_w[l] + x%tile_w[l]
  *
- * where p = y1*W + x1 is the query pixel.  One lookup window (2r+2)^2 then touches ~4.5 tiles of
- * 128 B (fp16) per level instead of 2r+2 cache-line rows, and the correlation GEMM's epilogue
- * writes every level as contiguous runs.  Padding elements inside edge tiles
- * hold unspecified values and are never read.
+ * with tiles_y[l] = level_h[l], tiles_x[l] = ceil(level_w[l] / tile_w[l]) and p = y1*W + x1 the
+ * query pixel.  Consecutive queries' chunks of the same target row are adjacent, so a wave of 64
+ * consecutive queries reads (lookup) and writes (GEMM epilogue) one row chunk as 64 x 16 B of
+ * contiguous memory.  Padding columns of a level's last chunk hold unspecified
+ * values and are never read.
  */
 typedef struct rmd_pyramid_desc {
     int batch, height, width;          /* query grid == level-0 target grid                  */
@@ -94,6 +96,63 @@ int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels,
  */
 int rmd_corr_lookup(const void* pyramid, const rmd_pyramid_desc* desc, const float* coords,
                     int radius, unsigned zero_level_mask, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);
+ * stack (B, d, d, 2C [+2], h, w) float32 contiguous with d = 2r+1, dim 1 the x-offset a-r and
+ * dim 2 the y-offset b-r — exactly the MatchingNet input (blocks/dicl.py:111-118).  h*w must be a
+ * multiple of 4 (MatchingNet already needs even h and w).
+ */
+
+/*
+ * Displacement stack with bilinear sampling.  Replaces the grid_sample/expand/cat of
+ * corr.dicl.CorrelationModule.forward (src/models/common/corr/dicl.py:26-54; dicl_1x1.py:51-79),
+ * of dicl_emb.py:51-89 (extra_delta = 1 appends the (a-r, b-r) channels) and the per-level gather
+ * of raft_dicl_ml.CorrelationModule.forward (src/models/impls/raft_dicl_ml.py:294-315):
+ *   stack[b,a,bb,0:C]  = fmap1
+ *   stack[b,a,bb,C:2C] = bilinear(fmap2, ((x/2^level + a-r) * (wl-1)/(norm_w-1),
+ *                                        (y/2^level + bb-r) * (hl-1)/(norm_h-1)))
+ * zero padding per tap.  corr/dicl.py: level 0, norm = (h, w) = (hl, wl); raft_dicl_ml level i:
+ * norm = fmap1's (h, w) (the reference normalises with the full-resolution size, :300-305).
+ */
+int rmd_dicl_stack(const float* fmap1, const float* fmap2, const float* coords, int batch, int channels,
+                   int height, int width, int level_height, int level_width, int radius, int level,
+                   int norm_height, int norm_width, int extra_delta, float* out, void* stream);
+
+/* Gradients of rmd_dicl_stack: grad_fmap1 = sum over displacements of the first C channels
+ * (deterministic); grad_fmap2 = bilinear scatter of channels C..2C-1 (float atomics, as ATen's
+ * grid_sampler_2d_backward).  Coordinates carry no gradient (they are detached, raft.py:402). */
+int rmd_dicl_stack_backward(const float* grad_stack, const float* coords, int batch, int channels,
+                            int height, int width, int level_height, int level_width, int radius,
+                            int level, int norm_height, int norm_width, int extra_delta,
+                            float* grad_fmap1, float* grad_fmap2, void* stream);
+
+/* Bytes of device workspace rmd_dicl_stack_int(_backward) needs (occlusion mask, 1 B/pixel). */
+size_t rmd_dicl_stack_int_workspace_bytes(int batch, int height, int width);
+
+/*
+ * DICL baseline integer matching volume with occlusion mask.  Replaces
+ * FlowLevel.compute_cost's volume build (src/models/impls/dicl.py:212-238): for di = i-ru (x),
+ * dj = j-rv (y), both halves are copied where (x+di, y+dj) is inside and zero elsewhere, then the
+ * whole 2C vector is zeroed where sum_c of its f2 half == 0.  out (B, 2ru+1, 2rv+1, 2C, h, w).
+ */
+int rmd_dicl_stack_int(const float* fmap1, const float* fmap2, int batch, int channels, int height, int width,
+                       int ru, int rv, float* out, void* workspace, void* stream);
+
+/* Gradients of rmd_dicl_stack_int (the mask is detached, dicl.py:236): deterministic gathers. */
+int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* fmap2, int batch, int channels,
+                                int height, int width, int ru, int rv, float* grad_fmap1,
+                                float* grad_fmap2, void* workspace, void* stream);
+
+/*
+ * Displacement-aware projection: out[b,o,p] = sum_i W[o,i] x[b,i,p] (1x1 conv, no bias) with
+ * W = conv1.weight[:,:,0,0] (D x D).  Replaces DisplacementAwareProjection.forward
+ * (src/models/common/blocks/dicl.py:143-150), the per-level DAPs of raft.py:146-168 and the
+ * 324x324 'full' DAP of raft_dicl_ml.py:268-273,339-341.  transpose = 1 applies W^T (the input
+ * gradient).  x, out: (B, D, pixels) float32.
+ */
+int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose, float* out,
+            void* stream);
 
 /* Message for the last failing call on this thread ("" if none). */
 const char* rmd_last_error(void);

@@ -18,7 +18,7 @@ void set_error(const char* fmt, ...) {
 
 void clear_error() { g_err[0] = '\0'; }
 
-static int level_tile(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
+static int level_chunk(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
 
 }  // namespace rmd
 
@@ -56,15 +56,15 @@ extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels
             rmd::set_error("rmd_pyramid_describe: level %d of a %dx%d map is empty", l, height, width);
             return RMD_ERR_SHAPE;
         }
-        const int t = rmd::level_tile(l);
+        const int t = rmd::level_chunk(l);
         d->level_h[l] = h;
         d->level_w[l] = w;
-        d->tile_h[l] = t;
+        d->tile_h[l] = 1;
         d->tile_w[l] = t;
-        d->tiles_y[l] = (h + t - 1) / t;
+        d->tiles_y[l] = h;
         d->tiles_x[l] = (w + t - 1) / t;
         d->level_offset[l] = off;
-        off += (long long)batch * d->tiles_y[l] * d->tiles_x[l] * n * t * t;
+        off += (long long)batch * d->tiles_y[l] * d->tiles_x[l] * n * t;
         h /= 2;
         w /= 2;
     }

@@ -6,13 +6,17 @@
 // window reads exactly the (2r+2)^2 integer patch [x0-r, x0+r+1] x [y0-r, y0+r+1] of p's own
 // level-i map.
 //
-// gfx950 design: one lane per query, 64 consecutive queries per wave so every
-// output store (one channel, 64 queries) is a coalesced 256-byte row of the (B, L*(2r+1)^2, H, W)
-// result.  Each patch row is fetched as whole tile rows (16 B for fp16 8x8 tiles) — 2 or 3
-// vector loads per row instead of 2r+2 scalar loads — and aligned with a log-step barrel shift
-// on packed 32-bit words.  Rows/columns outside the level are zero (grid_sample zero padding).
+// gfx950 design: one lane per (query, level), 64 consecutive queries per wave, so
+// every output store (one channel, 64 queries) is a coalesced 256-byte row of the
+// (B, L*(2r+1)^2, H, W) result.  Each patch row is fetched as whole row chunks (16 B for fp16 at
+// levels 0-1) — 2 or 3 vector loads per row instead of 2r+2 scalar loads — and aligned with a
+// log-step barrel shift on packed 32-bit words.  In the query-minor chunk layout (rmd.h) lanes
+// with similar flow read the same chunk of adjacent queries, i.e. contiguous memory.  Rows and
+// columns outside the level are zero (grid_sample zero padding).
 
 #include "rmd_common.h"
+
+#include <cstdlib>
 
 namespace rmd {
 namespace {
@@ -52,11 +56,13 @@ template <> __device__ __forceinline__ float word_elem<__half>(unsigned w, int i
     return __half2float(__ushort_as_half(s));
 }
 
-// One patch row (2R+2 values) of level L for this lane.  Columns outside [0, lw) are zero.
+// Load one patch row (2R+2 values) of a level whose tiles are TW wide.  Branch-free: the tile
+// chunks a row can span are fetched from clamped addresses (an unneeded chunk re-reads chunk 0's
+// line) and everything outside the level is zeroed with selects, so all loads of a patch issue
+// back to back.
 template <typename T, int R, int TW>
-__device__ __forceinline__ void load_row(const T* __restrict__ lvl_base, long long tile_row_base,
-                                         long long tile_stride, int tiles_x, int yin, int xs, int lw,
-                                         float (&v)[2 * R + 2]) {
+__device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long long tile_stride, int tiles_x, int xs,
+                                         int lw, bool row_ok, float (&v)[2 * R + 2]) {
     constexpr int S = sizeof(T);
     constexpr int EPW = 4 / S;                           // elements per 32-bit word
     constexpr int K = 2 * R + 2;                         // patch width
@@ -67,19 +73,16 @@ __device__ __forceinline__ void load_row(const T* __restrict__ lvl_base, long lo
     unsigned wd[NW + 1];
     const int tc0 = (xs >= 0) ? xs / TW : -((TW - 1 - xs) / TW);   // floor(xs / TW)
     const int sh = xs - tc0 * TW;                                   // 0 .. TW-1
+    const int tcl = min(max(tc0, 0), tiles_x - 1);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const int tc = tc0 + c;
-        if (tc >= 0 && tc < tiles_x && c * TW < sh + K) {
-            const T* p = lvl_base + tile_row_base + (long long)tc * tile_stride + yin * TW;
-            unsigned tmp[CW];
-            load_words<CW>(tmp, 0, reinterpret_cast<const unsigned char*>(p));
+        const bool need = tc >= 0 && tc < tiles_x && c * TW < sh + K;
+        const T* p = row_ptr + (long long)(need ? tc : tcl) * tile_stride;
+        unsigned tmp[CW];
+        load_words<CW>(tmp, 0, reinterpret_cast<const unsigned char*>(p));
 #pragma unroll
-            for (int i = 0; i < CW; ++i) wd[c * CW + i] = tmp[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < CW; ++i) wd[c * CW + i] = 0u;
-        }
+        for (int i = 0; i < CW; ++i) wd[c * CW + i] = need ? tmp[i] : 0u;
     }
     wd[NW] = 0u;
     // barrel shift left by sh elements: whole words first (log steps), then a half-word
@@ -87,33 +90,31 @@ __device__ __forceinline__ void load_row(const T* __restrict__ lvl_base, long lo
     constexpr int MAXW = (TW - 1) * S / 4;               // largest whole-word shift
 #pragma unroll
     for (int step = 1; step <= MAXW; step <<= 1) {
-        if (wsh & step) {
+        const bool on = (wsh & step) != 0;
 #pragma unroll
-            for (int i = 0; i < NW + 1; ++i) wd[i] = (i + step < NW + 1) ? wd[i + step] : 0u;
-        }
+        for (int i = 0; i < NW + 1; ++i) wd[i] = on ? ((i + step < NW + 1) ? wd[i + step] : 0u) : wd[i];
     }
     if constexpr (S == 2) {
-        if (sh & 1) {
+        const bool odd = (sh & 1) != 0;
 #pragma unroll
-            for (int i = 0; i < KW; ++i) wd[i] = __builtin_amdgcn_alignbyte(wd[i + 1], wd[i], 2);
-        }
+        for (int i = 0; i < KW; ++i) wd[i] = odd ? __builtin_amdgcn_alignbyte(wd[i + 1], wd[i], 2) : wd[i];
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const float e = word_elem<T>(wd[j / EPW], j % EPW);
         const int col = xs + j;
-        v[j] = (col >= 0 && col < lw) ? e : 0.f;
+        v[j] = (row_ok && col >= 0 && col < lw) ? e : 0.f;
     }
 }
 
-template <typename T, int R, int L>
+// ABL (diagnostic, RMD_ABLATE env, fp16/r=4 only): 0 normal, 1 = outputs to one channel slot
+// (no output HBM traffic), 2 = no pyramid loads (zero patch)
+template <typename T, int R, int L, int ABL = 0>
 __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const PyrGeom& g, int b, int p, int N,
-                                             float x, float y, unsigned zmask, float* __restrict__ outq,
+                                             float x, float y, unsigned zmask, float* __restrict__ o,
                                              bool active) {
     constexpr int D = 2 * R + 1;
     constexpr int K = 2 * R + 2;
-    constexpr int TL = level_tile(L);
-    float* o = outq + (size_t)L * D * D * N;
     const int lh = g.lh[L], lw = g.lw[L];
     if ((zmask >> L) & 1u) {
         if (active)
@@ -131,26 +132,27 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
     cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
     const float fx0 = floorf(cx), fy0 = floorf(cy);
     const float fx = cx - fx0, fy = cy - fy0;
-    const int x0 = (int)fx0, y0 = (int)fy0;
-    const int xs = x0 - R, ys = y0 - R;
-    const bool hit = active && xs <= lw - 1 && xs + K - 1 >= 0 && ys <= lh - 1 && ys + K - 1 >= 0;
+    const int xs = (int)fx0 - R, ys = (int)fy0 - R;
 
     const T* lvl = pyr + g.off[L];
-    const long long tile_stride = (long long)N * TL * TL;          // next tile column
-    const long long bq = (long long)b * g.ty[L];
+    constexpr int CW = level_chunk(L);                              // row-chunk width (elements)
+    const long long chunk_stride = (long long)N * CW;               // next chunk of the same row
+    const long long bq = (long long)b * lh;                         // tiles_y[L] == level height
+    const int txs = g.tx[L];
 
     float hprev[D];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const int yy = ys + j;
+        const bool row_ok = yy >= 0 && yy < lh;
+        const int yc = min(max(yy, 0), lh - 1);
+        const T* row_ptr = lvl + ((bq + yc) * txs) * chunk_stride + (long long)p * CW;
         float v[K];
-        if (hit && yy >= 0 && yy < lh) {
-            const int trow = yy / TL;
-            const long long row_base = ((bq + trow) * g.tx[L]) * tile_stride + (long long)p * TL * TL;
-            load_row<T, R, TL>(lvl, row_base, tile_stride, g.tx[L], yy - trow * TL, xs, lw, v);
-        } else {
+        if constexpr (ABL == 2) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) v[k] = 0.f;
+            for (int k = 0; k < K; ++k) v[k] = fx * (float)k;
+        } else {
+            load_row<T, R, CW>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
         }
         float hcur[D];
 #pragma unroll
@@ -158,40 +160,49 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
         if (j > 0 && active) {
             const int bb = j - 1;
 #pragma unroll
-            for (int a = 0; a < D; ++a) o[(size_t)(a * D + bb) * N] = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
+            for (int a = 0; a < D; ++a) o[ABL == 1 ? 0 : (size_t)(a * D + bb) * N] = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
         }
 #pragma unroll
         for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
     }
 }
 
-template <typename T, int R>
+// grid: (query blocks, batch, level) — one lane per (query, level)
+template <typename T, int R, int ABL = 0>
 __global__ void __launch_bounds__(kThreads)
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
     const int N = g.height * g.width;
-    const long long gid = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
     const int b = blockIdx.y;
-    const int p = (int)gid;
+    const int L = blockIdx.z;
     const bool active = p < N;
     const int pc = active ? p : N - 1;
     const float x = coords[((size_t)b * 2 + 0) * N + pc];
     const float y = coords[((size_t)b * 2 + 1) * N + pc];
     constexpr int D = 2 * R + 1;
-    float* outq = out + (size_t)b * g.levels * D * D * N + pc;
-    lookup_level<T, R, 0>(pyr, g, b, pc, N, x, y, zmask, outq, active);
-    if (g.levels > 1) lookup_level<T, R, 1>(pyr, g, b, pc, N, x, y, zmask, outq, active);
-    if (g.levels > 2) lookup_level<T, R, 2>(pyr, g, b, pc, N, x, y, zmask, outq, active);
-    if (g.levels > 3) lookup_level<T, R, 3>(pyr, g, b, pc, N, x, y, zmask, outq, active);
+    float* o = out + ((size_t)b * g.levels + L) * D * D * N + pc;
+    switch (L) {
+        case 0: lookup_level<T, R, 0, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 1: lookup_level<T, R, 1, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 2: lookup_level<T, R, 2, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        default: lookup_level<T, R, 3, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+    }
 }
 
 template <typename T>
 int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coords, int radius, unsigned zmask,
                   float* out, hipStream_t st) {
     const int N = d.height * d.width;
-    dim3 grid((N + kThreads - 1) / kThreads, d.batch);
+    dim3 grid((N + kThreads - 1) / kThreads, d.batch, d.levels);
     const T* p = reinterpret_cast<const T*>(pyr);
     const PyrGeom g = make_geom(d);
+    const char* abl_env = getenv("RMD_ABLATE");
+    const int abl = abl_env ? atoi(abl_env) : 0;
+    if constexpr (sizeof(T) == 2) {
+        if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+        if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+    }
     switch (radius) {
 #define RMD_CASE(RR) case RR: corr_lookup_kernel<T, RR><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)

@@ -3,29 +3,34 @@
 // Replaces raft.CorrBlock.__init__ (qzed/raft-meets-dicl src/models/impls/raft.py:18-47):
 //   corr0[b,p,q] = sum_c f1[b,c,p] f2[b,c,q] / sqrt(C);  level l = avg_pool2d(level l-1, 2, 2)
 //
-// gfx950 design:
-//  * one workgroup = 256 threads = 4 waves computes a 16x16 block of target pixels (256 targets,
-//    the MFMA "A"/row side) against 64 query pixels (the "B"/column side), K = C in 64-deep LDS
-//    chunks.  Wave w owns the 8x8 target sub-block (rows 8*(w>>1).., cols 8*(w&1)..) for all 64
-//    queries: 2x2 MFMA 32x32 tiles, one 32-target tile = 4 target rows x 8 target columns.
-//  * with targets on the MFMA rows, lane (h = lane>>5, j = lane&31) holds, for query j, an 8x4
-//    patch of target pixels (rows 0..7, cols 4h..4h+3 of the wave's 8x8 block), so the 2x2 pools
-//    for levels 1 and 2 are in-lane adds and level 3 needs one xor-32 lane exchange.
-//  * every level is written from the f32 accumulators (fp16 or fp32 storage) through a
-//    bank-swizzled LDS image as contiguous query-minor tile runs (see rmd.h for the layout).
-//  * compute = bf16 operands (v_mfma_f32_32x32x16_bf16) or exact f32 (v_mfma_f32_32x32x2_f32).
-//    Operands are first transposed to pixel-major, channel-contiguous (B, N, Cp) by a prep kernel
-//    so every fragment read is one 16-byte ds_read_b128.
+// gfx950 design.  Targets (fmap2 pixels) are the MFMA row side, queries (fmap1
+// pixels) the column side, and one 32-target MFMA tile is a 4 x 8 block of target pixels.  In the
+// 32x32 accumulator layout lane (h = lane>>5, j = lane&31) then holds, for query j, a 4-row x
+// 4-column patch of targets (columns 4h..4h+3) per tile, so the 2x2 average pools of levels 1-2
+// are in-lane adds and level 3 needs one xor-32 lane exchange.  Every level is written from the
+// f32 accumulators straight from registers into the query-minor row-chunk layout of rmd.h: the
+// lanes of a store instruction are consecutive queries, so each instruction writes whole
+// contiguous 512 B runs.
+//
+// Two kernels:
+//  * corr_pyramid_stationary — performance path (bf16 operands, fp16 pyramid, C = 256): a
+//    16x16 target block's A operand stays in LDS while 4 waves (one per SIMD, 512-register
+//    budget) sweep 32-query tiles with B fragments software-pipelined one tile ahead.
+//  * corr_pyramid_tiled — general path (exact f32 MFMA for parity, any C, f32 or fp16 storage):
+//    64 queries x 256 targets per workgroup, K staged through LDS in 64-deep chunks.
+// Operands are first transposed to pixel-major, channel-contiguous (B, N, Cp) by prep_operand.
 
 #include "rmd_common.h"
+
+#include <cstdlib>
 
 namespace rmd {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kBQ = 64;      // queries per workgroup
+constexpr int kBQ = 64;      // queries per workgroup (tiled kernel)
 constexpr int kNT = 256;     // targets per workgroup (16 x 16 block)
-constexpr int kKC = 64;      // K chunk staged in LDS
+constexpr int kKC = 64;      // K chunk staged in LDS (tiled kernel)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -37,10 +42,9 @@ template <> struct Operand<true> { using T = float; static constexpr int S = 4; 
 // padded staging row: kKC elements + 16 B -> ds_read_b128 fragment reads are conflict-free
 template <bool F32> constexpr int stage_stride() { return kKC * Operand<F32>::S + 16; }
 
-template <bool F32, typename TOut> constexpr int lds_bytes() {
-    constexpr int st = (kNT + kBQ) * stage_stride<F32>();
-    constexpr int ep = (4 * kBQ * 64 + kBQ * 64 + kBQ * 16 + kBQ * 4) * (int)sizeof(TOut);
-    return st > ep ? st : ep;
+// element offset of (b, query q, target row y, row-chunk x) at level l (rmd.h layout)
+__device__ __forceinline__ size_t lvl_index(const PyrGeom& g, int l, int b, int y, int xc, int q, int N) {
+    return (size_t)g.off[l] + ((((size_t)b * g.ty[l] + y) * g.tx[l] + xc) * N + q) * g.tw[l];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -69,55 +73,34 @@ prep_operand(const float* __restrict__ f, T* __restrict__ o, int C, int N, int C
     for (int j = 0; j < (int)(16 * sizeof(T) / 16); ++j) dst[j] = src[j];
 }
 
-// ---------------------------------------------------------------------------------------------
 template <typename TOut> __device__ __forceinline__ TOut cvt_out(float v);
 template <> __device__ __forceinline__ float cvt_out<float>(float v) { return v; }
 template <> __device__ __forceinline__ __half cvt_out<__half>(float v) { return __float2half_rn(v); }
 
-// write `n` (2 or 4) consecutive output elements at element offset `e` of query q's tile image
-// whose 16-byte chunks are XOR-swizzled by the query index (conflict-free ds_write / ds_read)
 template <typename TOut, int NE>
-__device__ __forceinline__ void img_put(unsigned char* img, int q, int tile_elems, int e,
-                                        const float* v) {
-    constexpr int S = sizeof(TOut);
-    const int cq = tile_elems * S / 16;                   // 16-B chunks per query tile
-    const int byte = e * S;
-    const int chunk = (byte >> 4) ^ (q & (cq - 1));
-    unsigned char* p = img + (size_t)(q * cq + chunk) * 16 + (byte & 15);
+__device__ __forceinline__ void put(TOut* p, const float* v) {
     TOut tmp[NE];
 #pragma unroll
     for (int i = 0; i < NE; ++i) tmp[i] = cvt_out<TOut>(v[i]);
-    if constexpr (NE * S == 16) {
-        *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(tmp);
-    } else if constexpr (NE * S == 8) {
-        *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(tmp);
-    } else {
-        static_assert(NE * S == 4, "unsupported image write");
-        *reinterpret_cast<unsigned*>(p) = *reinterpret_cast<const unsigned*>(tmp);
-    }
+    constexpr int NB = NE * sizeof(TOut);
+    if constexpr (NB == 16) *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(tmp);
+    else if constexpr (NB == 8) *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(tmp);
+    else if constexpr (NB == 4) *reinterpret_cast<unsigned*>(p) = *reinterpret_cast<const unsigned*>(tmp);
+    else *p = tmp[0];
 }
 
-// copy nq queries' swizzled tile images (16-B chunks) to a contiguous global run
-__device__ __forceinline__ void img_store(const unsigned char* img, unsigned char* dst, int nq,
-                                          int cq, int worker, int nworkers) {
-    const int total = nq * cq;
-    for (int id = worker; id < total; id += nworkers) {
-        const int q = id / cq, c = id - q * cq;
-        const uint4 v = *reinterpret_cast<const uint4*>(img + (size_t)(q * cq + (c ^ (q & (cq - 1)))) * 16);
-        *reinterpret_cast<uint4*>(dst + (size_t)id * 16) = v;
-    }
-}
-
+// ---------------------------------------------------------------------------------------------
+// General tiled kernel.  Workgroup = 4 waves = 16x16 targets x 64 queries; wave w owns the 8x8
+// target sub-block (rows 8*(w>>1).., cols 8*(w&1)..) for all 64 queries (2x2 MFMA 32x32 tiles).
 template <bool F32, typename TOut>
 __global__ void __launch_bounds__(kThreads)
-corr_pyramid_kernel(const typename Operand<F32>::T* __restrict__ opA,   // fmap2 (B, N, Cp)
-                    const typename Operand<F32>::T* __restrict__ opB,   // fmap1 (B, N, Cp)
-                    int Cp, float scale, PyrGeom g, TOut* __restrict__ pyr) {
+corr_pyramid_tiled(const typename Operand<F32>::T* __restrict__ opA,   // fmap2 (B, N, Cp)
+                   const typename Operand<F32>::T* __restrict__ opB,   // fmap1 (B, N, Cp)
+                   int Cp, float scale, PyrGeom g, TOut* __restrict__ pyr) {
     using T = typename Operand<F32>::T;
     constexpr int S = Operand<F32>::S;
     constexpr int SS = stage_stride<F32>();
     constexpr int PPR = kKC * S / 16;                       // 16-B pieces per staged row
-    constexpr int SO = sizeof(TOut);
 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* sA = smem;
@@ -149,7 +132,6 @@ corr_pyramid_kernel(const typename Operand<F32>::T* __restrict__ opA,   // fmap2
     for (int tr = 0; tr < 2; ++tr) arow[tr] = (8 * (w >> 1) + 4 * tr + (r >> 3)) * 16 + 8 * (w & 1) + (r & 7);
 
     for (int kc = 0; kc < Cp; kc += kKC) {
-        // ---- stage the A (targets) and B (queries) chunk into LDS -----------------------------
 #pragma unroll 4
         for (int i = 0; i < kNT * PPR / kThreads; ++i) {
             const int id = tid + kThreads * i, row = id / PPR, pc = id - row * PPR;
@@ -169,7 +151,6 @@ corr_pyramid_kernel(const typename Operand<F32>::T* __restrict__ opA,   // fmap2
         }
         __syncthreads();
 
-        // ---- MFMA over the chunk ------------------------------------------------------------
         if constexpr (!F32) {
 #pragma unroll
             for (int s = 0; s < kKC / 16; ++s) {
@@ -207,85 +188,315 @@ corr_pyramid_kernel(const typename Operand<F32>::T* __restrict__ opA,   // fmap2
         __syncthreads();
     }
 
-    // ---- epilogue: scale, pool, write LDS images ----------------------------------------------
-    unsigned char* img0 = smem;                                   // [4 waves][64 q][64 el]
-    unsigned char* img1 = img0 + 4 * kBQ * 64 * SO;               // [64 q][64 el]   (8x8 tile)
-    unsigned char* img2 = img1 + kBQ * 64 * SO;                   // [64 q][16 el]   (4x4 tile)
-    unsigned char* img3 = img2 + kBQ * 16 * SO;                   // [64 q][4 el]    (2x2 tile)
+    // ---- epilogue: scale, pool in-lane, store each level's row pieces from registers ------------
     const int levels = g.levels;
-
 #pragma unroll
     for (int tq = 0; tq < 2; ++tq) {
-        const int q = 32 * tq + r;
+        const int q = q0 + 32 * tq + r;
+        if (q >= N) continue;
         float o[8][4];                                            // rows 0..7, cols 4h..4h+3
 #pragma unroll
         for (int tr = 0; tr < 2; ++tr)
 #pragma unroll
             for (int e = 0; e < 16; ++e) o[4 * tr + (e >> 2)][e & 3] = acc[tr][tq][e] * scale;
-        unsigned char* im0 = img0 + (size_t)w * kBQ * 64 * SO;
+        // level 0: wave block rows 16rb + 8(w>>1) + row, chunk 2cb + (w&1), elements 4h..4h+3
+        {
+            const int xc = 2 * cb + (w & 1);
+            if (xc < g.tx[0]) {
 #pragma unroll
-        for (int row = 0; row < 8; ++row) img_put<TOut, 4>(im0, q, 64, row * 8 + 4 * h, o[row]);
-        if (levels > 1) {
-            float l1[4][2];
-#pragma unroll
-            for (int yy = 0; yy < 4; ++yy)
-#pragma unroll
-                for (int xx = 0; xx < 2; ++xx)
-                    l1[yy][xx] = 0.25f * ((o[2 * yy][2 * xx] + o[2 * yy][2 * xx + 1]) +
-                                          (o[2 * yy + 1][2 * xx] + o[2 * yy + 1][2 * xx + 1]));
-#pragma unroll
-            for (int yy = 0; yy < 4; ++yy)
-                img_put<TOut, 2>(img1, q, 64, (4 * (w >> 1) + yy) * 8 + 4 * (w & 1) + 2 * h, l1[yy]);
-            if (levels > 2) {
-                float l2[2];
-#pragma unroll
-                for (int yy = 0; yy < 2; ++yy)
-                    l2[yy] = 0.25f * ((l1[2 * yy][0] + l1[2 * yy][1]) + (l1[2 * yy + 1][0] + l1[2 * yy + 1][1]));
-                TOut* im2 = reinterpret_cast<TOut*>(img2) + q * 16;
-#pragma unroll
-                for (int yy = 0; yy < 2; ++yy) im2[(2 * (w >> 1) + yy) * 4 + 2 * (w & 1) + h] = cvt_out<TOut>(l2[yy]);
-                if (levels > 3) {
-                    float s3 = l2[0] + l2[1];
-                    s3 += __shfl_xor(s3, 32);
-                    if (h == 0) reinterpret_cast<TOut*>(img3)[q * 4 + (w >> 1) * 2 + (w & 1)] = cvt_out<TOut>(0.25f * s3);
+                for (int row = 0; row < 8; ++row) {
+                    const int y = 16 * rb + 8 * (w >> 1) + row;
+                    if (y < g.ty[0]) put<TOut, 4>(pyr + lvl_index(g, 0, b, y, xc, q, N) + 4 * h, o[row]);
                 }
             }
         }
+        if (levels < 2) continue;
+        float l1[4][2];
+#pragma unroll
+        for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+            for (int xx = 0; xx < 2; ++xx)
+                l1[yy][xx] = 0.25f * ((o[2 * yy][2 * xx] + o[2 * yy][2 * xx + 1]) +
+                                      (o[2 * yy + 1][2 * xx] + o[2 * yy + 1][2 * xx + 1]));
+        if (cb < g.tx[1]) {
+#pragma unroll
+            for (int yy = 0; yy < 4; ++yy) {
+                const int y = 8 * rb + 4 * (w >> 1) + yy;
+                if (y < g.ty[1]) put<TOut, 2>(pyr + lvl_index(g, 1, b, y, cb, q, N) + 4 * (w & 1) + 2 * h, l1[yy]);
+            }
+        }
+        if (levels < 3) continue;
+        float l2[2];
+#pragma unroll
+        for (int yy = 0; yy < 2; ++yy)
+            l2[yy] = 0.25f * ((l1[2 * yy][0] + l1[2 * yy][1]) + (l1[2 * yy + 1][0] + l1[2 * yy + 1][1]));
+        if (cb < g.tx[2]) {
+#pragma unroll
+            for (int yy = 0; yy < 2; ++yy) {
+                const int y = 4 * rb + 2 * (w >> 1) + yy;
+                if (y < g.ty[2]) put<TOut, 1>(pyr + lvl_index(g, 2, b, y, cb, q, N) + 2 * (w & 1) + h, &l2[yy]);
+            }
+        }
+        if (levels < 4) continue;
+        float s3 = l2[0] + l2[1];
+        s3 += __shfl_xor(s3, 32);
+        s3 *= 0.25f;
+        const int y3 = 2 * rb + (w >> 1);
+        if (h == 0 && cb < g.tx[3] && y3 < g.ty[3]) put<TOut, 1>(pyr + lvl_index(g, 3, b, y3, cb, q, N) + (w & 1), &s3);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Target-stationary kernel (bf16 operands, fp16 pyramid, C = 256): the performance path.
+//
+// One workgroup = 4 waves (one per SIMD) owns a 16x16 block of target pixels: its A operand
+// (256 targets x 256 bf16 = 128 KiB) is loaded into LDS once, 16-B chunks XOR-swizzled by row so the
+// 16 rows a ds_read_b128 lane group reads hit distinct banks.  Each wave sweeps 32-query tiles:
+// 8 MFMA 32x32x16 tiles per k-step (all 256 targets x 32 queries), then pools in-lane and stores
+// every level straight from registers.  v_permlane32_swap pairs the two half-waves' 8-byte row
+// halves into full 16-byte row chunks, so one store instruction writes two contiguous 512-byte runs.
+constexpr int kSThreads = 256;
+constexpr int kSWaves = kSThreads / 64;
+constexpr int kStoresPerTile = 23;    // 16 (L0) + 4 (L1) + 2 (L2) + 1 (L3) per lane per 32-query tile
+
+__device__ __forceinline__ unsigned pack_half2(float a, float b) {
+    const __half2 h = __floats2half2_rn(a, b);
+    return *reinterpret_cast<const unsigned*>(&h);
+}
+
+__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+
+struct SCtx {
+    int b, rb, cb, N;
+    float scale;
+};
+
+// B-fragment loads in inline asm, retired by ONE hand-placed `s_waitcnt vmcnt(kStoresPerTile)`:
+// between a tile's loads and that wait the wave issues exactly kStoresPerTile compiler stores (the
+// epilogue, every store unconditional) and no other vector-memory op (no compiler-visible global
+// loads in the loop, no spills: checked in the .s by tests/test_asm_audit.py), so the wait retires
+// the loads while the previous tile's stores stay in flight.  hipcc does not count asm loads, so
+// it never inserts its own draining vmcnt(0).
+__device__ __forceinline__ void s_load_b_asm(bf16x8 (&bq)[16], const __bf16* src) {
+#define RMD_GLD(S) asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(bq[S]) : "v"(src), "i"((S) * 32) : "memory")
+    RMD_GLD(0); RMD_GLD(1); RMD_GLD(2); RMD_GLD(3); RMD_GLD(4); RMD_GLD(5); RMD_GLD(6); RMD_GLD(7);
+    RMD_GLD(8); RMD_GLD(9); RMD_GLD(10); RMD_GLD(11); RMD_GLD(12); RMD_GLD(13); RMD_GLD(14); RMD_GLD(15);
+#undef RMD_GLD
+}
+
+template <int N>
+__device__ __forceinline__ void s_wait_b(bf16x8 (&bq)[16]) {
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]), "+v"(bq[6]),
+                   "+v"(bq[7]), "+v"(bq[8]), "+v"(bq[9]), "+v"(bq[10]), "+v"(bq[11]), "+v"(bq[12]), "+v"(bq[13]),
+                   "+v"(bq[14]), "+v"(bq[15])
+                 : "i"(N)
+                 : "memory");
+}
+
+__device__ __forceinline__ void s_mma(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
+                                      const int (&arow)[8], int h) {
+    constexpr int Cp = 256, SWZ = 15;
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[ti][e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+#pragma unroll
+        for (int ti = 0; ti < 8; ++ti) {
+            const int row = arow[ti];
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * Cp * 2 + (((2 * s + h) ^ (row & SWZ)) << 4));
+            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[s], acc[ti], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // bound the A-fragment look-ahead (register budget)
+    }
+}
+
+// Every store is unconditional: an invalid one (query past N, row or chunk outside a level, a
+// level beyond g.levels) is redirected to this lane's 16-B trash slot, so each tile issues exactly
+// kStoresPerTile stores (see s_load_b_asm).  ABL is a diagnostic ablation (RMD_ABLATE env):
+// 1 = every store to trash (no HBM write traffic).
+template <int ABL>
+__device__ __forceinline__ __half* sel(bool ok, __half* p, __half* trash) { return (ok && ABL != 1) ? p : trash; }
+
+template <int ABL>
+__device__ __forceinline__ void s_epilogue(const f32x16 (&acc)[8], const SCtx& c, const PyrGeom& g, int q, int h,
+                                           __half* __restrict__ pyr, __half* __restrict__ trash) {
+    const bool qv = q < c.N;
+    const int N = c.N, b = c.b, rb = c.rb, cb = c.cb;
+    const float scale = c.scale;
+    // V(row 0..15, cg 0..1, k 0..3) = level-0 value at target row, col 8cg + 4h + k
+#define V(row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)] * scale)
+    // level 0: rows 16rb + 8tr + 2m + h after the swap; chunk 2cb + tc
+#pragma unroll
+    for (int tr = 0; tr < 2; ++tr) {
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc) {
+            const int xc = 2 * cb + tc;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int r0 = 8 * tr + 2 * m;
+                unsigned x0 = pack_half2(V(r0, tc, 0), V(r0, tc, 1));
+                unsigned x1 = pack_half2(V(r0, tc, 2), V(r0, tc, 3));
+                unsigned y0 = pack_half2(V(r0 + 1, tc, 0), V(r0 + 1, tc, 1));
+                unsigned y1 = pack_half2(V(r0 + 1, tc, 2), V(r0 + 1, tc, 3));
+                swap32(x0, y0);
+                swap32(x1, y1);
+                const int y = 16 * rb + r0 + h;
+                const bool ok = qv && y < g.ty[0] && xc < g.tx[0];
+                *reinterpret_cast<uint4*>(sel<ABL>(ok, pyr + lvl_index(g, 0, b, min(y, g.ty[0] - 1), xc, q, N), trash)) =
+                    make_uint4(x0, x1, y0, y1);
+            }
+        }
+    }
+    // level 1: one 8x8 block; lane h holds cols {2h, 2h+1} (cg 0) and {4+2h, 5+2h} (cg 1)
+    float l1[8][2][2];
+#pragma unroll
+    for (int yy = 0; yy < 8; ++yy)
+#pragma unroll
+        for (int cg = 0; cg < 2; ++cg)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                l1[yy][cg][u] = 0.25f * ((V(2 * yy, cg, 2 * u) + V(2 * yy, cg, 2 * u + 1)) +
+                                         (V(2 * yy + 1, cg, 2 * u) + V(2 * yy + 1, cg, 2 * u + 1)));
+#undef V
+    const bool l1ok = qv && g.levels > 1 && cb < g.tx[1];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        unsigned x0 = pack_half2(l1[2 * m][0][0], l1[2 * m][0][1]);
+        unsigned x1 = pack_half2(l1[2 * m][1][0], l1[2 * m][1][1]);
+        unsigned y0 = pack_half2(l1[2 * m + 1][0][0], l1[2 * m + 1][0][1]);
+        unsigned y1 = pack_half2(l1[2 * m + 1][1][0], l1[2 * m + 1][1][1]);
+        swap32(x0, y0);
+        swap32(x1, y1);
+        const int y = 8 * rb + 2 * m + h;
+        *reinterpret_cast<uint4*>(sel<ABL>(l1ok && y < g.ty[1], pyr + lvl_index(g, 1, b, min(y, g.ty[1] - 1), cb, q, N), trash)) =
+            make_uint4(x0, y0, x1, y1);
+    }
+    // level 2: one 4x4 block; lane h holds cols {h, 2+h}; lane h stores rows 2h and 2h+1 (8 B each)
+    float l2[4][2];
+#pragma unroll
+    for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+        for (int cg = 0; cg < 2; ++cg)
+            l2[yy][cg] = 0.25f * ((l1[2 * yy][cg][0] + l1[2 * yy][cg][1]) + (l1[2 * yy + 1][cg][0] + l1[2 * yy + 1][cg][1]));
+    {
+        unsigned mine[4], other[4];
+#pragma unroll
+        for (int yy = 0; yy < 4; ++yy) {
+            mine[yy] = pack_half2(l2[yy][0], l2[yy][1]);          // (col h, col 2+h)
+            other[yy] = __shfl_xor(mine[yy], 32);
+        }
+        const bool l2ok = qv && g.levels > 2 && cb < g.tx[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            // row 2h+k, selected with compile-time indices (a runtime index would go to scratch)
+            const unsigned mk = h ? mine[2 + k] : mine[k];
+            const unsigned ok_ = h ? other[2 + k] : other[k];
+            const unsigned e0 = h ? ok_ : mk;      // cols 0 and 2 (held by h = 0)
+            const unsigned e1 = h ? mk : ok_;      // cols 1 and 3 (held by h = 1)
+            const int y = 4 * rb + 2 * h + k;
+            *reinterpret_cast<uint2*>(sel<ABL>(l2ok && y < g.ty[2], pyr + lvl_index(g, 2, b, min(y, g.ty[2] - 1), cb, q, N), trash)) =
+                make_uint2((e0 & 0xffffu) | (e1 << 16), (e0 >> 16) | (e1 & 0xffff0000u));
+        }
+    }
+    // level 3: one 2x2 block; lane h stores row h (4 B)
+    {
+        float p3[2][2];
+#pragma unroll
+        for (int yy = 0; yy < 2; ++yy)
+#pragma unroll
+            for (int cg = 0; cg < 2; ++cg) {
+                const float s_ = l2[2 * yy][cg] + l2[2 * yy + 1][cg];
+                p3[yy][cg] = 0.25f * (s_ + __shfl_xor(s_, 32));
+            }
+        const int y = 2 * rb + h;
+        const bool ok = qv && g.levels > 3 && cb < g.tx[3] && y < g.ty[3];
+        const unsigned v = h ? pack_half2(p3[1][0], p3[1][1]) : pack_half2(p3[0][0], p3[0][1]);
+        *reinterpret_cast<unsigned*>(sel<ABL>(ok, pyr + lvl_index(g, 3, b, min(y, g.ty[3] - 1), cb, q, N), trash)) = v;
+    }
+}
+
+// ABL (diagnostic, RMD_ABLATE env): 0 = normal, 1 = every store to trash, 2 = no MFMA
+template <int ABL>
+__global__ void __launch_bounds__(kSThreads, 1)
+corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, float scale, PyrGeom g,
+                        int qsplit, __half* __restrict__ pyr, __half* __restrict__ trash_base) {
+    constexpr int Cp = 256, CPR = Cp / 8, SWZ = 15;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int H = g.height, W = g.width, N = H * W;
+    const int ncb = (W + 15) >> 4;
+    const int nblk = ((H + 15) >> 4) * ncb;
+    // XCD-aware bijective remap: consecutive logical blocks (same batch) share an XCD's L2
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tb = lid % nblk;
+    const int rest = lid / nblk;
+    const int split = rest % qsplit;
+    const int b = rest / qsplit;
+    const int rb = tb / ncb, cb = tb - rb * ncb;
+    const int ty0 = rb * 16, tx0 = cb * 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);    // wave-uniform: scalar loop control
+    const int j = lane & 31, h = lane >> 5;
+    __half* trash = trash_base + lane * 8;            // 16 B per lane (stores of all waves may collide)
+
+    // ---- A block -> LDS (zero rows for targets outside the image) ------------------------------
+    const __bf16* gA = opA + (size_t)b * N * Cp;
+    for (int id = tid; id < 256 * CPR; id += kSThreads) {
+        const int row = id / CPR, c = id - row * CPR;
+        const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
+        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ (row & SWZ)) << 4)) = v;
     }
     __syncthreads();
 
-    // ---- contiguous query-minor tile runs -> HBM -----------------------------------------------
-    const int nq = min(kBQ, N - q0);
-    {
-        const int trow = 2 * rb + (w >> 1), tcol = 2 * cb + (w & 1);
-        if (trow < g.ty[0] && tcol < g.tx[0]) {
-            const size_t base = (size_t)g.off[0] + (((size_t)b * g.ty[0] + trow) * g.tx[0] + tcol) * N * 64 + (size_t)q0 * 64;
-            img_store(img0 + (size_t)w * kBQ * 64 * SO, reinterpret_cast<unsigned char*>(pyr + base), nq,
-                      64 * SO / 16, lane, 64);
-        }
+    int arow[8];
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti) arow[ti] = (4 * (ti >> 1) + (j >> 3)) * 16 + 8 * (ti & 1) + (j & 7);
+
+    SCtx c;
+    c.b = b; c.rb = rb; c.cb = cb; c.N = N; c.scale = scale;
+
+    const __bf16* gB = opB + (size_t)b * N * Cp;
+    const int nqt = (N + 31) >> 5;
+    const int stride = kSWaves * qsplit;
+    int qt = split * kSWaves + w;
+    if (qt >= nqt) return;
+    // software pipeline: tile t+1's B fragments load while tile t's MFMAs and epilogue run
+    bf16x8 b0[16], b1[16];
+    f32x16 acc[8];
+    const int last = nqt - 1;
+    const size_t hoff = 8 * h;
+    s_load_b_asm(b0, gB + (size_t)min(qt * 32 + j, N - 1) * Cp + hoff);
+    s_wait_b<0>(b0);
+    while (true) {
+        const int qn = qt + stride;
+        s_load_b_asm(b1, gB + (size_t)min(min(qn, last) * 32 + j, N - 1) * Cp + hoff);
+        if constexpr (ABL != 2) s_mma(acc, b0, smem, arow, h);
+        else for (int ti = 0; ti < 8; ++ti) for (int e = 0; e < 16; ++e) acc[ti][e] = b0[0][0] * 0.f;
+        s_epilogue<ABL>(acc, c, g, qt * 32 + j, h, pyr, trash);
+        s_wait_b<kStoresPerTile>(b1);
+        if (qn >= nqt) break;
+        const int qn2 = qn + stride;
+        s_load_b_asm(b0, gB + (size_t)min(min(qn2, last) * 32 + j, N - 1) * Cp + hoff);
+        if constexpr (ABL != 2) s_mma(acc, b1, smem, arow, h);
+        else for (int ti = 0; ti < 8; ++ti) for (int e = 0; e < 16; ++e) acc[ti][e] = b1[0][0] * 0.f;
+        s_epilogue<ABL>(acc, c, g, qn * 32 + j, h, pyr, trash);
+        s_wait_b<kStoresPerTile>(b0);
+        if (qn2 >= nqt) break;
+        qt = qn2;
     }
-    if (levels > 1 && rb < g.ty[1] && cb < g.tx[1]) {
-        const size_t base = (size_t)g.off[1] + (((size_t)b * g.ty[1] + rb) * g.tx[1] + cb) * N * 64 + (size_t)q0 * 64;
-        img_store(img1, reinterpret_cast<unsigned char*>(pyr + base), nq, 64 * SO / 16, tid, kThreads);
-    }
-    if (levels > 2 && rb < g.ty[2] && cb < g.tx[2]) {
-        const size_t base = (size_t)g.off[2] + (((size_t)b * g.ty[2] + rb) * g.tx[2] + cb) * N * 16 + (size_t)q0 * 16;
-        const uint4* src = reinterpret_cast<const uint4*>(img2);
-        uint4* dst = reinterpret_cast<uint4*>(pyr + base);
-        for (int id = tid; id < nq * 16 * SO / 16; id += kThreads) dst[id] = src[id];
-    }
-    if (levels > 3 && rb < g.ty[3] && cb < g.tx[3]) {
-        const size_t base = (size_t)g.off[3] + (((size_t)b * g.ty[3] + rb) * g.tx[3] + cb) * N * 4 + (size_t)q0 * 4;
-        if constexpr (SO == 2) {
-            const uint2* src = reinterpret_cast<const uint2*>(img3);
-            uint2* dst = reinterpret_cast<uint2*>(pyr + base);
-            for (int id = tid; id < nq; id += kThreads) dst[id] = src[id];
-        } else {
-            const uint4* src = reinterpret_cast<const uint4*>(img3);
-            uint4* dst = reinterpret_cast<uint4*>(pyr + base);
-            for (int id = tid; id < nq; id += kThreads) dst[id] = src[id];
-        }
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <bool F32, typename TOut>
@@ -301,12 +512,39 @@ int launch_pyramid(const float* f1, const float* f2, int C, const rmd_pyramid_de
     prep_operand<T><<<pg, kThreads, 0, st>>>(f1, opB, C, N, Cp);
     int rc = check_launch("rmd_corr_pyramid/prep");
     if (rc) return rc;
-    constexpr int lds = lds_bytes<F32, TOut>();
-    auto kern = corr_pyramid_kernel<F32, TOut>;
+    const float scale = 1.0f / sqrtf((float)C);
+    const PyrGeom geom = make_geom(d);
+    if constexpr (!F32 && sizeof(TOut) == 2) {
+        if (Cp == 256 && !getenv("RMD_FORCE_TILED_GEMM")) {
+            const int nblk = ((d.height + 15) / 16) * ((d.width + 15) / 16);
+            const int nqt = (N + 31) / 32;
+            int qsplit = 1;
+            while (nblk * d.batch * qsplit < 256 && qsplit * kSWaves * 4 <= nqt) qsplit *= 2;
+            const int lds = 256 * Cp * 2;
+            const int nwg = nblk * d.batch * qsplit;
+            __half* out = reinterpret_cast<__half*>(pyramid);
+            __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * N * Cp);
+            const char* abl_env = getenv("RMD_ABLATE");
+            const int abl = abl_env ? atoi(abl_env) : 0;
+            switch (abl) {
+#define RMD_SCASE(ABL)                                                                                          \
+    case ABL:                                                                                                   \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<ABL>),                  \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);                             \
+        corr_pyramid_stationary<ABL><<<nwg, kSThreads, lds, st>>>(opA, opB, scale, geom, qsplit, out, trash);   \
+        break;
+                RMD_SCASE(1) RMD_SCASE(2)
+                default: RMD_SCASE(0)
+#undef RMD_SCASE
+            }
+            return check_launch("rmd_corr_pyramid/gemm-stationary");
+        }
+    }
+    constexpr int lds = (kNT + kBQ) * stage_stride<F32>();
+    auto kern = corr_pyramid_tiled<F32, TOut>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     dim3 grid((N + kBQ - 1) / kBQ, ((d.height + 15) / 16) * ((d.width + 15) / 16), d.batch);
-    const float scale = 1.0f / sqrtf((float)C);
-    kern<<<grid, kThreads, lds, st>>>(opA, opB, Cp, scale, make_geom(d), reinterpret_cast<TOut*>(pyramid));
+    kern<<<grid, kThreads, lds, st>>>(opA, opB, Cp, scale, geom, reinterpret_cast<TOut*>(pyramid));
     return check_launch("rmd_corr_pyramid/gemm");
 }
 
@@ -317,7 +555,7 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     if (!d || channels <= 0) return 0;
     const size_t Cp = (size_t)(channels + rmd::kKC - 1) / rmd::kKC * rmd::kKC;
     const size_t es = compute == RMD_F32 ? 4 : 2;
-    return 2 * (size_t)d->batch * d->height * d->width * Cp * es;
+    return 2 * (size_t)d->batch * d->height * d->width * Cp * es + 1024;   // + 64 lanes x 16 B trash
 }
 
 extern "C" int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,

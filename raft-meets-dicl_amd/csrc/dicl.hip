@@ -1,0 +1,382 @@
+// dicl.hip — DICL displacement-invariant cost-volume construction and displacement-aware projection.
+//
+// Replaces (qzed/raft-meets-dicl v2):
+//  * corr.dicl.CorrelationModule.forward gather/expand/cat  src/models/common/corr/dicl.py:26-54
+//    (same in dicl_1x1.py:51-79; dicl_emb.py:51-89 adds the 2 displacement channels) and the
+//    per-level gather of raft_dicl_ml.CorrelationModule.forward (src/models/impls/raft_dicl_ml.py:294-315)
+//    -> rmd_dicl_stack / rmd_dicl_stack_backward
+//  * FlowLevel.compute_cost volume build + occlusion mask   src/models/impls/dicl.py:212-238
+//    -> rmd_dicl_stack_int / rmd_dicl_stack_int_backward
+//  * DisplacementAwareProjection 1x1 conv                    src/models/common/blocks/dicl.py:121-150
+//    -> rmd_dap (forward; with transpose = 1 it is the input gradient W^T g)
+//
+// All of them are HBM-bound byte movers: one lane owns 4 consecutive pixels of one
+// displacement plane, so every store is a 16-byte-per-lane, fully coalesced row of the contiguous
+// (B, du, dv, 2C(+2), h, w) MatchingNet input; the f1 half is re-read from L2 per displacement.
+
+#include "rmd_common.h"
+
+namespace rmd {
+namespace {
+
+constexpr int kThreads = 256;
+
+// bilinear, align_corners=True, zero padding per tap: the 4 taps of one sample position
+struct Taps {
+    int idx[4];
+    float wgt[4];
+};
+
+__device__ __forceinline__ Taps make_taps(float px, float py, int hl, int wl) {
+    Taps t;
+    px = fminf(fmaxf(px, -1.0e6f), 1.0e6f);
+    py = fminf(fmaxf(py, -1.0e6f), 1.0e6f);
+    const float fx0 = floorf(px), fy0 = floorf(py);
+    const float fx = px - fx0, fy = py - fy0;
+    const int x0 = (int)fx0, y0 = (int)fy0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int xx = x0 + (k & 1), yy = y0 + (k >> 1);
+        const bool ok = xx >= 0 && xx < wl && yy >= 0 && yy < hl;
+        const float wx = (k & 1) ? fx : 1.f - fx;
+        const float wy = (k >> 1) ? fy : 1.f - fy;
+        t.idx[k] = ok ? yy * wl + xx : 0;
+        t.wgt[k] = ok ? wx * wy : 0.f;
+    }
+    return t;
+}
+
+// sample position of displacement (a, bb) for pixel p: the reference adds the integer offset to
+// coords/2^level, normalises with (wn-1),(hn-1) and grid_sample un-normalises with (wl-1),(hl-1)
+struct StackParams {
+    int B, C, h, w, hl, wl, radius, extra;     // extra = 2 adds the displacement channels (dicl_emb)
+    float inv_scale;                            // 1 / 2^level
+    float sx, sy;                               // (wl-1)/(wn-1), (hl-1)/(hn-1)
+};
+
+// grid: (pixel quads, d*d, B); one lane = 4 consecutive pixels of one displacement plane
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_kernel(const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
+                  StackParams P, float* __restrict__ out) {
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int quad = blockIdx.x * kThreads + threadIdx.x;
+    const int p0 = quad * 4;
+    if (p0 >= n) return;
+    const int d = 2 * P.radius + 1;
+    const int disp = blockIdx.y;                 // a * d + bb
+    const int a = disp / d, bb = disp - a * d;
+    const int b = blockIdx.z;
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const float* cx = coords + (size_t)b * 2 * n;
+    const float* cy = cx + n;
+    Taps t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = p0 + k;
+        const float px = (cx[p] * P.inv_scale + (float)(a - P.radius)) * P.sx;
+        const float py = (cy[p] * P.inv_scale + (float)(bb - P.radius)) * P.sy;
+        t[k] = make_taps(px, py, P.hl, P.wl);
+    }
+    float* o = out + ((size_t)(b * d * d + disp) * C2) * n + p0;
+    const float* f1b = f1 + (size_t)b * C * n + p0;
+    const float* f2b = f2 + (size_t)b * C * nl;
+    for (int c = 0; c < C; ++c) {
+        *reinterpret_cast<float4*>(o + (size_t)c * n) = *reinterpret_cast<const float4*>(f1b + (size_t)c * n);
+        const float* f2c = f2b + (size_t)c * nl;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = t[k].wgt[0] * f2c[t[k].idx[0]] + t[k].wgt[1] * f2c[t[k].idx[1]] +
+                   t[k].wgt[2] * f2c[t[k].idx[2]] + t[k].wgt[3] * f2c[t[k].idx[3]];
+        *reinterpret_cast<float4*>(o + (size_t)(C + c) * n) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    if (P.extra) {       // dicl_emb.py:81-85: delta (dx = a-r, dy = bb-r) as two constant channels
+        const float dx = (float)(a - P.radius), dy = (float)(bb - P.radius);
+        *reinterpret_cast<float4*>(o + (size_t)(2 * C) * n) = make_float4(dx, dx, dx, dx);
+        *reinterpret_cast<float4*>(o + (size_t)(2 * C + 1) * n) = make_float4(dy, dy, dy, dy);
+    }
+}
+
+// backward: grad_f1 = sum over displacements of the f1 half (deterministic, no atomics)
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_grad_f1_kernel(const float* __restrict__ g, StackParams P, float* __restrict__ gf1) {
+    const int n = P.h * P.w;
+    const int quad = blockIdx.x * kThreads + threadIdx.x;
+    const int p0 = quad * 4;
+    if (p0 >= n) return;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const int d = 2 * P.radius + 1, C2 = 2 * P.C + P.extra;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* gp = g + ((size_t)b * d * d * C2 + c) * n + p0;
+    for (int disp = 0; disp < d * d; ++disp) {
+        const float4 v = *reinterpret_cast<const float4*>(gp + (size_t)disp * C2 * n);
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    *reinterpret_cast<float4*>(gf1 + ((size_t)b * P.C + c) * n + p0) = s;
+}
+
+// backward: grad_f2 = bilinear scatter of the f2 half (float atomics, like grid_sampler backward)
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                          float* __restrict__ gf2) {
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= n) return;
+    const int d = 2 * P.radius + 1;
+    const int disp = blockIdx.y;
+    const int a = disp / d, bb = disp - a * d;
+    const int b = blockIdx.z;
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const float px = (coords[(size_t)b * 2 * n + p] * P.inv_scale + (float)(a - P.radius)) * P.sx;
+    const float py = (coords[(size_t)b * 2 * n + n + p] * P.inv_scale + (float)(bb - P.radius)) * P.sy;
+    const Taps t = make_taps(px, py, P.hl, P.wl);
+    const float* gp = g + ((size_t)(b * d * d + disp) * C2 + C) * n + p;
+    float* gb = gf2 + (size_t)b * C * nl;
+    for (int c = 0; c < C; ++c) {
+        const float gv = gp[(size_t)c * n];
+        float* gc = gb + (size_t)c * nl;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (t.wgt[k] != 0.f) atomicAdd(gc + t.idx[k], gv * t.wgt[k]);
+    }
+}
+
+// ---- DICL baseline integer volume ------------------------------------------------------------
+struct IntParams {
+    int B, C, h, w, ru, rv;
+};
+
+// occlusion mask of dicl.py:236-237 depends only on the displaced f2 pixel: nz = sum_c f2 != 0
+__global__ void __launch_bounds__(kThreads)
+dicl_nz_kernel(const float* __restrict__ f2, IntParams P, unsigned char* __restrict__ nz) {
+    const int n = P.h * P.w;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= n) return;
+    const int b = blockIdx.y;
+    const float* f = f2 + (size_t)b * P.C * n + p;
+    float s = 0.f;
+    for (int c = 0; c < P.C; ++c) s += f[(size_t)c * n];
+    nz[(size_t)b * n + p] = s != 0.f;
+}
+
+// grid: (pixels/4 per row chunk, du*dv, B); lane = 4 consecutive pixels of one displacement plane
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_int_kernel(const float* __restrict__ f1, const float* __restrict__ f2,
+                      const unsigned char* __restrict__ nz, IntParams P, float* __restrict__ out) {
+    const int n = P.h * P.w;
+    const int quad = blockIdx.x * kThreads + threadIdx.x;
+    const int p0 = quad * 4;
+    if (p0 >= n) return;
+    const int dv = 2 * P.rv + 1;
+    const int disp = blockIdx.y;                 // i * dv + j
+    const int i = disp / dv, jj = disp - i * dv;
+    const int di = i - P.ru, dj = jj - P.rv;
+    const int b = blockIdx.z;
+    const int C = P.C;
+    int src[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = p0 + k;
+        const int y = p / P.w, x = p - y * P.w;
+        const int xx = x + di, yy = y + dj;
+        const bool inb = xx >= 0 && xx < P.w && yy >= 0 && yy < P.h;
+        src[k] = inb ? yy * P.w + xx : 0;
+        ok[k] = inb && nz[(size_t)b * n + src[k]];
+    }
+    const int du_dv = (2 * P.ru + 1) * dv;
+    float* o = out + ((size_t)(b * du_dv + disp) * 2 * C) * n + p0;
+    const float* f1b = f1 + (size_t)b * C * n + p0;
+    const float* f2b = f2 + (size_t)b * C * n;
+    for (int c = 0; c < C; ++c) {
+        const float4 a = *reinterpret_cast<const float4*>(f1b + (size_t)c * n);
+        const float* f2c = f2b + (size_t)c * n;
+        *reinterpret_cast<float4*>(o + (size_t)c * n) =
+            make_float4(ok[0] ? a.x : 0.f, ok[1] ? a.y : 0.f, ok[2] ? a.z : 0.f, ok[3] ? a.w : 0.f);
+        *reinterpret_cast<float4*>(o + (size_t)(C + c) * n) =
+            make_float4(ok[0] ? f2c[src[0]] : 0.f, ok[1] ? f2c[src[1]] : 0.f, ok[2] ? f2c[src[2]] : 0.f,
+                        ok[3] ? f2c[src[3]] : 0.f);
+    }
+}
+
+// backward (deterministic gathers, no atomics):
+//   grad_f1[c, p] = sum_{i,j} ok_ij(p) g[i,j,c,p];   grad_f2[c, q] = sum_{i,j} ok_ij(q-d_ij) g[i,j,C+c,q-d_ij]
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_int_backward_kernel(const float* __restrict__ g, const unsigned char* __restrict__ nz, IntParams P,
+                               float* __restrict__ gf1, float* __restrict__ gf2) {
+    const int n = P.h * P.w;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= n) return;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const int C = P.C;
+    const int du = 2 * P.ru + 1, dv = 2 * P.rv + 1;
+    const int y = p / P.w, x = p - y * P.w;
+    const unsigned char* nzb = nz + (size_t)b * n;
+    const bool nzp = nzb[p];
+    const float* gb = g + (size_t)b * du * dv * 2 * C * n;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < du; ++i) {
+        for (int jj = 0; jj < dv; ++jj) {
+            const int di = i - P.ru, dj = jj - P.rv;
+            const size_t plane = (size_t)(i * dv + jj) * 2 * C;
+            // this pixel as the query: its f1 half (needs target p + d in bounds and non-zero)
+            const int xx = x + di, yy = y + dj;
+            if (xx >= 0 && xx < P.w && yy >= 0 && yy < P.h && nzb[yy * P.w + xx]) s1 += gb[(plane + c) * n + p];
+            // this pixel as the target of query p - d: its f2 half
+            const int qx = x - di, qy = y - dj;
+            if (nzp && qx >= 0 && qx < P.w && qy >= 0 && qy < P.h) s2 += gb[(plane + C + c) * n + qy * P.w + qx];
+        }
+    }
+    gf1[((size_t)b * C + c) * n + p] = s1;
+    gf2[((size_t)b * C + c) * n + p] = s2;
+}
+
+// ---- displacement-aware projection: out[b, o, p] = sum_i W[o, i] x[b, i, p] ------------------
+// One lane per pixel, 16 output channels per pass held in registers; W rows broadcast from LDS.
+constexpr int kDapOB = 16;
+
+template <bool LDS_W>
+__global__ void __launch_bounds__(kThreads)
+dap_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
+           float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float sw[];     // D x D (row o, col i)
+    if constexpr (LDS_W) {
+        for (int k = threadIdx.x; k < D * D; k += kThreads) {
+            const int o = k / D, i = k - o * D;
+            sw[k] = transpose ? wgt[i * D + o] : wgt[k];
+        }
+        __syncthreads();
+    }
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    if (p >= n) return;
+    const float* xb = x + (size_t)b * D * n + p;
+    float* ob = out + (size_t)b * D * n + p;
+    for (int o0 = 0; o0 < D; o0 += kDapOB) {
+        float acc[kDapOB];
+#pragma unroll
+        for (int k = 0; k < kDapOB; ++k) acc[k] = 0.f;
+        for (int i = 0; i < D; ++i) {
+            const float xv = xb[(size_t)i * n];
+#pragma unroll
+            for (int k = 0; k < kDapOB; ++k) {
+                const int o = min(o0 + k, D - 1);
+                float wv;
+                if constexpr (LDS_W) wv = sw[o * D + i];
+                else wv = transpose ? wgt[i * D + o] : wgt[o * D + i];     // wave-uniform: scalar loads
+                acc[k] = fmaf(wv, xv, acc[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kDapOB; ++k)
+            if (o0 + k < D) ob[(size_t)(o0 + k) * n] = acc[k];
+    }
+}
+
+int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int radius, int level, int nh, int nw,
+                 int extra) {
+    RMD_REQUIRE(B > 0 && C > 0 && h > 0 && w > 0 && hl > 0 && wl > 0, RMD_ERR_SHAPE, "rmd_dicl_stack: bad sizes");
+    RMD_REQUIRE(radius >= 0 && radius <= 32, RMD_ERR_SHAPE, "rmd_dicl_stack: radius %d out of range", radius);
+    RMD_REQUIRE((h * w) % 4 == 0, RMD_ERR_SHAPE, "rmd_dicl_stack: h*w must be a multiple of 4 (MatchingNet needs even h, w)");
+    RMD_REQUIRE(level >= 0 && level < 16, RMD_ERR_SHAPE, "rmd_dicl_stack: bad level");
+    P.B = B; P.C = C; P.h = h; P.w = w; P.hl = hl; P.wl = wl; P.radius = radius; P.extra = extra ? 2 : 0;
+    P.inv_scale = 1.0f / (float)(1 << level);
+    // (wl-1)/(wn-1): 0/0 -> NaN exactly as the reference's normalisation does for 1-pixel maps
+    P.sx = (float)(wl - 1) / (float)(nw - 1);
+    P.sy = (float)(hl - 1) / (float)(nh - 1);
+    return RMD_OK;
+}
+
+}  // namespace
+}  // namespace rmd
+
+using namespace rmd;
+
+extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const float* coords, int batch, int channels,
+                              int height, int width, int level_height, int level_width, int radius, int level,
+                              int norm_height, int norm_width, int extra_delta, float* out, void* stream) {
+    RMD_REQUIRE(fmap1 && fmap2 && coords && out, RMD_ERR_ARG, "rmd_dicl_stack: null pointer");
+    StackParams P;
+    int rc = stack_params(P, batch, channels, height, width, level_height, level_width, radius, level, norm_height,
+                          norm_width, extra_delta);
+    if (rc) return rc;
+    const int d = 2 * radius + 1;
+    dim3 grid((height * width / 4 + kThreads - 1) / kThreads, d * d, batch);
+    dicl_stack_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
+    return check_launch("rmd_dicl_stack");
+}
+
+extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coords, int batch, int channels,
+                                       int height, int width, int level_height, int level_width, int radius,
+                                       int level, int norm_height, int norm_width, int extra_delta,
+                                       float* grad_fmap1, float* grad_fmap2, void* stream) {
+    RMD_REQUIRE(grad_stack && coords && grad_fmap1 && grad_fmap2, RMD_ERR_ARG, "rmd_dicl_stack_backward: null pointer");
+    StackParams P;
+    int rc = stack_params(P, batch, channels, height, width, level_height, level_width, radius, level, norm_height,
+                          norm_width, extra_delta);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const int d = 2 * radius + 1;
+    dim3 g1((height * width / 4 + kThreads - 1) / kThreads, channels, batch);
+    dicl_stack_grad_f1_kernel<<<g1, kThreads, 0, st>>>(grad_stack, P, grad_fmap1);
+    (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
+    dim3 g2((height * width + kThreads - 1) / kThreads, d * d, batch);
+    dicl_stack_grad_f2_kernel<<<g2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap2);
+    return check_launch("rmd_dicl_stack_backward");
+}
+
+extern "C" size_t rmd_dicl_stack_int_workspace_bytes(int batch, int height, int width) {
+    return (size_t)batch * height * width;
+}
+
+extern "C" int rmd_dicl_stack_int(const float* fmap1, const float* fmap2, int batch, int channels, int height,
+                                  int width, int ru, int rv, float* out, void* workspace, void* stream) {
+    RMD_REQUIRE(fmap1 && fmap2 && out && workspace, RMD_ERR_ARG, "rmd_dicl_stack_int: null pointer");
+    RMD_REQUIRE(batch > 0 && channels > 0 && height > 0 && width > 0 && ru >= 0 && rv >= 0, RMD_ERR_SHAPE,
+                "rmd_dicl_stack_int: bad sizes");
+    RMD_REQUIRE((height * width) % 4 == 0, RMD_ERR_SHAPE, "rmd_dicl_stack_int: h*w must be a multiple of 4");
+    IntParams P{batch, channels, height, width, ru, rv};
+    hipStream_t st = as_stream(stream);
+    const int n = height * width;
+    unsigned char* nz = reinterpret_cast<unsigned char*>(workspace);
+    dicl_nz_kernel<<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(fmap2, P, nz);
+    dim3 grid((n / 4 + kThreads - 1) / kThreads, (2 * ru + 1) * (2 * rv + 1), batch);
+    dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, fmap2, nz, P, out);
+    return check_launch("rmd_dicl_stack_int");
+}
+
+extern "C" int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* fmap2, int batch, int channels,
+                                           int height, int width, int ru, int rv, float* grad_fmap1,
+                                           float* grad_fmap2, void* workspace, void* stream) {
+    RMD_REQUIRE(grad_mvol && fmap2 && grad_fmap1 && grad_fmap2 && workspace, RMD_ERR_ARG,
+                "rmd_dicl_stack_int_backward: null pointer");
+    RMD_REQUIRE(batch > 0 && channels > 0 && height > 0 && width > 0 && ru >= 0 && rv >= 0, RMD_ERR_SHAPE,
+                "rmd_dicl_stack_int_backward: bad sizes");
+    IntParams P{batch, channels, height, width, ru, rv};
+    hipStream_t st = as_stream(stream);
+    const int n = height * width;
+    unsigned char* nz = reinterpret_cast<unsigned char*>(workspace);
+    dicl_nz_kernel<<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(fmap2, P, nz);
+    dim3 grid((n + kThreads - 1) / kThreads, channels, batch);
+    dicl_stack_int_backward_kernel<<<grid, kThreads, 0, st>>>(grad_mvol, nz, P, grad_fmap1, grad_fmap2);
+    return check_launch("rmd_dicl_stack_int_backward");
+}
+
+extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose,
+                       float* out, void* stream) {
+    RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");
+    RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap: bad sizes");
+    const size_t lds = sizeof(float) * (size_t)disp * disp;
+    dim3 grid((pixels + kThreads - 1) / kThreads, batch);
+    if (lds <= 64 * 1024) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_kernel<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        dap_kernel<true><<<grid, kThreads, lds, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
+    } else {   // e.g. the 324x324 'full' DAP of raft_dicl_ml: W streamed through the scalar cache
+        dap_kernel<false><<<grid, kThreads, 0, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
+    }
+    return check_launch("rmd_dap");
+}

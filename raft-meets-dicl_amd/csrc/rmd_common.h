@@ -61,9 +61,9 @@ inline PyrGeom make_geom(const rmd_pyramid_desc& d) {
     return g;
 }
 
-// tile edge of level l: 8, 8, 4, 2 — a 16x16 level-0 target block maps to whole tiles on
-// every level
-__host__ __device__ constexpr int level_tile(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
+// row-chunk width of level l: 8, 8, 4, 2 elements — the 16 target columns of a GEMM workgroup
+// map to whole chunks on every level
+__host__ __device__ constexpr int level_chunk(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

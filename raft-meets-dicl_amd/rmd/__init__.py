@@ -6,7 +6,7 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.raft.CorrBlock      <- src/models/impls/raft.py:15-95
 """
 
-from . import ops, raft  # noqa: F401
+from . import blocks, corr, dicl, ops, raft  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

@@ -64,12 +64,12 @@ class Pyramid:
         """Level i in the reference layout (B, H, W, 1, H_i, W_i) as float32 — for tests/debugging."""
         d = self.desc
         b, h, w = d.batch, d.height, d.width
-        th, tw, ty, tx = d.tile_h[i], d.tile_w[i], d.tiles_y[i], d.tiles_x[i]
+        cw, nc = d.tile_w[i], d.tiles_x[i]
         hl, wl = d.level_h[i], d.level_w[i]
         n = h * w
         off = d.level_offset[i]
-        x = self.data[off: off + b * ty * tx * n * th * tw].view(b, ty, tx, n, th, tw)
-        x = x.permute(0, 3, 1, 4, 2, 5).reshape(b, n, ty * th, tx * tw)[:, :, :hl, :wl]
+        x = self.data[off: off + b * hl * nc * n * cw].view(b, hl, nc, n, cw)
+        x = x.permute(0, 3, 1, 2, 4).reshape(b, n, hl, nc * cw)[..., :wl]
         return x.float().reshape(b, h, w, 1, hl, wl)
 
 
@@ -110,3 +110,133 @@ def corr_lookup(pyr, coords, radius, mask_costs=()):
         _lib.check(_lib.lib().rmd_corr_lookup(_ptr(pyr.data), ctypes.byref(d), _ptr(co), radius, mask, _ptr(out),
                                               _lib.stream_ptr(co.device)), "rmd_corr_lookup")
     return out
+
+
+# ---- DICL cost volumes and DAP ------------------------------------------------------------------
+
+def _stream(t):
+    return _lib.stream_ptr(t.device)
+
+
+class _DiclStack(torch.autograd.Function):
+    """stack = [f1 expanded | bilinear(f2, coords/2^level + delta)] — corr/dicl.py:26-54."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, coords, radius, level, norm_hw, extra_delta):
+        _require_gpu(f1, f2, coords)
+        f1c = f1.detach().float().contiguous()
+        f2c = f2.detach().float().contiguous()
+        co = coords.detach().float().contiguous()
+        b, c, h, w = f1c.shape
+        hl, wl = f2c.shape[-2:]
+        if f2c.shape[:2] != (b, c) or tuple(co.shape) != (b, 2, h, w):
+            raise ValueError("dicl_stack: fmap2 must be (B,C,hl,wl) and coords (B,2,h,w) matching fmap1")
+        nh, nw = norm_hw if norm_hw is not None else (h, w)
+        d = 2 * radius + 1
+        out = torch.empty((b, d, d, 2 * c + (2 if extra_delta else 0), h, w), dtype=torch.float32,
+                          device=f1c.device)
+        with torch.cuda.device(f1c.device):
+            _lib.check(_lib.lib().rmd_dicl_stack(_ptr(f1c), _ptr(f2c), _ptr(co), b, c, h, w, hl, wl, radius, level,
+                                                 nh, nw, int(bool(extra_delta)), _ptr(out), _stream(f1c)),
+                       "rmd_dicl_stack")
+        ctx.save_for_backward(co)
+        ctx.meta = (b, c, h, w, hl, wl, radius, level, nh, nw, int(bool(extra_delta)))
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (co,) = ctx.saved_tensors
+        b, c, h, w, hl, wl, radius, level, nh, nw, extra = ctx.meta
+        g = grad.float().contiguous()
+        g1 = torch.empty((b, c, h, w), dtype=torch.float32, device=g.device)
+        g2 = torch.empty((b, c, hl, wl), dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            _lib.check(_lib.lib().rmd_dicl_stack_backward(_ptr(g), _ptr(co), b, c, h, w, hl, wl, radius, level, nh,
+                                                          nw, extra, _ptr(g1), _ptr(g2), _stream(g)),
+                       "rmd_dicl_stack_backward")
+        return g1, g2, None, None, None, None, None
+
+
+def dicl_stack(fmap1, fmap2, coords, radius, level=0, norm_hw=None, extra_delta=False):
+    """(B,C,h,w), (B,C,hl,wl), (B,2,h,w) -> (B, 2r+1, 2r+1, 2C[+2], h, w) MatchingNet input."""
+    return _DiclStack.apply(fmap1, fmap2, coords, radius, level, norm_hw, extra_delta)
+
+
+class _DiclStackInt(torch.autograd.Function):
+    """Integer-displacement matching volume with occlusion mask — impls/dicl.py:212-238."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, ru, rv):
+        _require_gpu(f1, f2)
+        f1c = f1.detach().float().contiguous()
+        f2c = f2.detach().float().contiguous()
+        b, c, h, w = f1c.shape
+        if tuple(f2c.shape) != (b, c, h, w):
+            raise ValueError("dicl_stack_int: fmap1 and fmap2 must have equal (B,C,h,w) shapes")
+        lib = _lib.lib()
+        ws = torch.empty(lib.rmd_dicl_stack_int_workspace_bytes(b, h, w), dtype=torch.uint8, device=f1c.device)
+        out = torch.empty((b, 2 * ru + 1, 2 * rv + 1, 2 * c, h, w), dtype=torch.float32, device=f1c.device)
+        with torch.cuda.device(f1c.device):
+            _lib.check(lib.rmd_dicl_stack_int(_ptr(f1c), _ptr(f2c), b, c, h, w, ru, rv, _ptr(out), _ptr(ws),
+                                              _stream(f1c)), "rmd_dicl_stack_int")
+        ctx.save_for_backward(f2c)
+        ctx.meta = (b, c, h, w, ru, rv)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (f2c,) = ctx.saved_tensors
+        b, c, h, w, ru, rv = ctx.meta
+        g = grad.float().contiguous()
+        lib = _lib.lib()
+        ws = torch.empty(lib.rmd_dicl_stack_int_workspace_bytes(b, h, w), dtype=torch.uint8, device=g.device)
+        g1 = torch.empty((b, c, h, w), dtype=torch.float32, device=g.device)
+        g2 = torch.empty((b, c, h, w), dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            _lib.check(lib.rmd_dicl_stack_int_backward(_ptr(g), _ptr(f2c), b, c, h, w, ru, rv, _ptr(g1), _ptr(g2),
+                                                       _ptr(ws), _stream(g)), "rmd_dicl_stack_int_backward")
+        return g1, g2, None, None
+
+
+def dicl_stack_int(fmap1, fmap2, ru, rv):
+    return _DiclStackInt.apply(fmap1, fmap2, ru, rv)
+
+
+class _Dap(torch.autograd.Function):
+    """out[b,o,p] = sum_i W[o,i] x[b,i,p] — blocks/dicl.py:143-150 (1x1 conv, no bias)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        _require_gpu(x, weight)
+        b, dd = x.shape[:2]
+        xc = x.detach().float().contiguous()
+        wc = weight.detach().float().reshape(dd, dd).contiguous()
+        n = xc.numel() // (b * dd)
+        out = torch.empty_like(xc)
+        with torch.cuda.device(xc.device):
+            _lib.check(_lib.lib().rmd_dap(_ptr(xc), _ptr(wc), b, dd, n, 0, _ptr(out), _stream(xc)), "rmd_dap")
+        ctx.save_for_backward(xc, wc)
+        ctx.wshape = weight.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        xc, wc = ctx.saved_tensors
+        b, dd = xc.shape[:2]
+        n = xc.numel() // (b * dd)
+        g = grad.float().contiguous()
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(g)
+            with torch.cuda.device(g.device):
+                _lib.check(_lib.lib().rmd_dap(_ptr(g), _ptr(wc), b, dd, n, 1, _ptr(gx), _stream(g)), "rmd_dap^T")
+        gw = None
+        if ctx.needs_input_grad[1]:
+            # plain library GEMM (hipBLASLt): dW = sum_b g_b x_b^T
+            gw = torch.matmul(g.view(b, dd, n), xc.view(b, dd, n).transpose(1, 2)).sum(0).reshape(ctx.wshape)
+        return gx, gw
+
+
+def dap(x, weight):
+    """x (B, D, ...) -> W x over the displacement dim; weight (D, D[, 1, 1])."""
+    return _Dap.apply(x, weight)

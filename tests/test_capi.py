@@ -36,11 +36,12 @@ def test_describe_cfg2_geometry():
     d = _lib.describe(8, 55, 128, 4, _lib.RMD_F16)
     assert [d.level_h[i] for i in range(4)] == [55, 27, 13, 6]
     assert [d.level_w[i] for i in range(4)] == [128, 64, 32, 16]
-    assert [d.tile_h[i] for i in range(4)] == [8, 8, 4, 2]
-    assert [d.tiles_y[i] for i in range(4)] == [7, 4, 4, 3]
+    assert [d.tile_h[i] for i in range(4)] == [1, 1, 1, 1]
+    assert [d.tile_w[i] for i in range(4)] == [8, 8, 4, 2]
+    assert [d.tiles_y[i] for i in range(4)] == [55, 27, 13, 6]
     assert [d.tiles_x[i] for i in range(4)] == [16, 8, 8, 8]
     n = 55 * 128
-    sizes = [7 * 16 * 64, 4 * 8 * 64, 4 * 8 * 16, 3 * 8 * 4]
+    sizes = [55 * 128, 27 * 64, 13 * 32, 6 * 16]
     assert d.total_elements == 8 * n * sum(sizes)
     assert [d.level_offset[i] for i in range(4)] == [0] + [8 * n * sum(sizes[:i]) for i in range(1, 4)]
 

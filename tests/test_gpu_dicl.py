@@ -1,0 +1,144 @@
+"""GPU parity of the DICL cost volumes and DAP (rmd_dicl_stack*, rmd_dap) against reference
+golden vectors (tests/golden) and the float64 oracle.
+
+Tolerances (max-normalised, conftest.rel_max_err): stacks 1e-5 (bilinear in pixel coordinates vs
+the reference's [-1,1] round trip), integer volume bit-exact (pure copy + mask), DAP 1e-5,
+full modules through MatchingNet (MIOpen convolutions) 1e-4.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import load_golden, rel_max_err
+from detinit import det_init
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a, grad=False):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV).requires_grad_(grad)
+
+
+def test_dicl_stack_forward_backward_golden():
+    import rmd
+    g = load_golden("dicl_b1_c16_8x12")
+    f1, f2 = _t(g["fmap1"], True), _t(g["fmap2"], True)
+    st = rmd.ops.dicl_stack(f1, f2, _t(g["coords"]), int(g["radius"]))
+    assert tuple(st.shape) == g["stack"].shape and st.is_contiguous()
+    assert rel_max_err(st.detach().cpu().numpy(), g["stack"]) < 1e-5
+    g1, g2 = torch.autograd.grad(st, (f1, f2), _t(g["grad_stack"]))
+    assert rel_max_err(g1.cpu().numpy(), g["grad_fmap1"]) < 1e-5
+    assert rel_max_err(g2.cpu().numpy(), g["grad_fmap2"]) < 1e-5
+
+
+def test_dicl_correlation_module_golden():
+    """Whole drop-in module (gather -> MatchingNet -> DAP) with the reference's weights/state keys."""
+    import rmd
+    g = load_golden("dicl_b1_c16_8x12")
+    mod = rmd.corr.make_cmod("dicl", 16, int(g["radius"]), dap_init="standard")
+    assert sorted(mod.state_dict().keys()) == sorted(g["sd.keys"].tolist())
+    det_init(mod)
+    mod = mod.to(DEV).eval()
+    cap = {}
+    mod.mnet.register_forward_hook(lambda m, i, o: cap.update(cost=o))
+    with torch.no_grad():
+        out = mod(_t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"]), dap=True)
+    assert rel_max_err(cap["cost"].cpu().numpy(), g["cost"]) < 1e-4
+    assert rel_max_err(out.cpu().numpy(), g["out"]) < 1e-4
+
+
+@pytest.mark.parametrize("dap_type", ["separate", "full"])
+def test_dicl_ml_level_stacks_golden(dap_type):
+    import rmd
+    g = load_golden(f"ml_{dap_type}_b1_c8_8x12")
+    co = _t(g["coords"])
+    h, w = g["coords"].shape[-2:]
+    for i in range(int(g["levels"])):
+        f2 = g[f"fmap2_{i}"]
+        st = rmd.ops.dicl_stack(_t(g[f"fmap1_{i}"]), _t(f2), co, int(g["radius"]), level=i, norm_hw=(h, w))
+        assert rel_max_err(st.cpu().numpy(), g[f"stack_{i}"]) < 1e-5
+
+
+def test_dicl_emb_stack_has_delta_channels():
+    import rmd
+    g = load_golden("dicl_b1_c16_8x12")
+    st = rmd.ops.dicl_stack(_t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"]), 4, extra_delta=True).cpu().numpy()
+    assert st.shape[3] == 2 * 16 + 2
+    assert rel_max_err(st[:, :, :, :32], g["stack"]) < 1e-5
+    a = np.arange(9)[:, None] - 4
+    assert np.array_equal(st[0, :, :, 32, 0, 0], np.broadcast_to(a, (9, 9)).astype(np.float32))
+    assert np.array_equal(st[0, :, :, 33, 0, 0], np.broadcast_to(a.T, (9, 9)).astype(np.float32))
+
+
+def test_dicl_stack_cfg4_shape_vs_oracle():
+    """KITTI ctf-l3 1/16 level (24x80), C=32, r=4, B=2, fractional smooth flow."""
+    import rmd
+    rng = np.random.default_rng(4)
+    b, c, h, w = 2, 32, 24, 80
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    co = (np.stack([xs, ys])[None] + rng.normal(0, 3, (b, 2, h, w))).astype(np.float32)
+    st = rmd.ops.dicl_stack(_t(f1), _t(f2), _t(co), 4).cpu().numpy()
+    ref = oracle.dicl_stack(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64), 4)
+    assert rel_max_err(st, ref) < 1e-5
+
+
+def test_dicl_stack_int_golden_bit_exact():
+    import rmd
+    g = load_golden("dicl_cost_b2_c16_10x12")
+    ru, rv = g["maxdisp"].tolist()
+    f1, f2 = _t(g["fmap1"], True), _t(g["fmap2"], True)
+    mvol = rmd.ops.dicl_stack_int(f1, f2, ru, rv)
+    assert np.array_equal(mvol.detach().cpu().numpy(), g["mvol"])
+    g1, g2 = torch.autograd.grad(mvol, (f1, f2), _t(g["grad_mvol"]))
+    assert rel_max_err(g1.cpu().numpy(), g["grad_fmap1"]) < 1e-6
+    assert rel_max_err(g2.cpu().numpy(), g["grad_fmap2"]) < 1e-6
+
+
+def test_dicl_compute_cost_golden():
+    import rmd
+    g = load_golden("dicl_cost_b2_c16_10x12")
+    mnet = rmd.blocks.dicl.MatchingNet(32)
+    assert sorted(mnet.state_dict().keys()) == sorted(g["sd.keys"].tolist())
+    mnet = det_init(mnet).to(DEV).eval()
+    with torch.no_grad():
+        cost = rmd.dicl.compute_cost(mnet, _t(g["fmap1"]), _t(g["fmap2"]), g["maxdisp"].tolist())
+    assert rel_max_err(cost.cpu().numpy(), g["cost"]) < 1e-4
+
+
+def test_dicl_stack_int_cfg3_level2_vs_oracle():
+    """DICL baseline level-2 shape of cfg3 (96x128), C=32, 7x7, with zero holes."""
+    import rmd
+    rng = np.random.default_rng(8)
+    b, c, h, w = 1, 32, 96, 128
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2[:, :, 10:20, 30:50] = 0
+    mvol = rmd.ops.dicl_stack_int(_t(f1), _t(f2), 3, 3).cpu().numpy()
+    assert np.array_equal(mvol, oracle.dicl_stack_int(f1, f2, 3, 3))
+
+
+def test_dap_golden():
+    import rmd
+    g = load_golden("dap_b2_r4_6x8")
+    x = _t(g["x"], True)
+    wt = _t(g["weight"], True)
+    y = rmd.ops.dap(x, wt)
+    assert rel_max_err(y.detach().cpu().numpy(), g["out"]) < 1e-5
+    gx, gw = torch.autograd.grad(y, (x, wt), _t(g["grad_out"]))
+    assert rel_max_err(gx.cpu().numpy(), g["grad_x"]) < 1e-5
+    assert rel_max_err(gw.cpu().numpy(), g["grad_weight"]) < 1e-5
+
+
+def test_dap_full_324_vs_oracle():
+    """'full' DAP of raft_dicl_ml (324x324, weight streamed, not LDS-resident)."""
+    import rmd
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((2, 324, 12, 16)).astype(np.float32)
+    wt = (rng.standard_normal((324, 324, 1, 1)) * 0.05).astype(np.float32)
+    y = rmd.ops.dap(_t(x), _t(wt)).cpu().numpy()
+    assert rel_max_err(y, oracle.dap(x.astype(np.float64), wt.astype(np.float64))) < 1e-5
