@@ -13,8 +13,9 @@ Metric: frame-pairs/s over the whole job (all ranks).  One process per GPU (torc
 pairs are independent, so each rank runs its own batch of 8 ("weak" scaling, no data-path
 collective; timing is max over ranks via one all_reduce after the timed region).
 
-Also reported: roofline of the dominant kernel (the lookup: 12 launches/step), measured live with
-HIP events on the launch stream, plus the correlation GEMM's MFMA fraction, and the CPU oracle
+Also reported: roofline of the dominant kernel per step (GEMM: one launch; lookup: 12 launches),
+measured live with HIP events on the launch stream (the GEMM launch alone, the 12 lookups as one
+bracket), both kernels' rooflines and the GEMM's MFMA fraction, and the CPU oracle
 (test infrastructure, numpy/BLAS float32 restatement of the reference path) timed on a bounded
 sample on this host, rank 0 only.
 """
@@ -121,28 +122,21 @@ def main():
     f1, f2, coords = synthetic(B, args.channels, h8, w8, args.iters, 1234 + rank, device)
 
     stream = torch.cuda.current_stream(device)
-    ev_corr = []
-    ev_look = []
+    ev_gemm = []      # (start, end) around the GEMM launch alone (rmd_corr_pyramid_prepared)
+    ev_look = []      # (start, end) around the 12 lookup launches of a step
 
     def step(record):
+        pyr = ops.corr_pyramid(f1, f2, args.levels, args.precision, events=ev_gemm if record else None)
         if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        pyr = ops.corr_pyramid(f1, f2, args.levels, args.precision)
-        if record:
-            e1.record(stream)
-            ev_corr.append((e0, e1))
+            a = torch.cuda.Event(enable_timing=True)
+            z = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
         out = None
         for it in range(args.iters):
-            if record:
-                a = torch.cuda.Event(enable_timing=True)
-                z = torch.cuda.Event(enable_timing=True)
-                a.record(stream)
             out = ops.corr_lookup(pyr, coords[it], args.radius)
-            if record:
-                z.record(stream)
-                ev_look.append((a, z))
+        if record:
+            z.record(stream)
+            ev_look.append((a, z))
         return out
 
     for _ in range(args.warmup):
@@ -161,25 +155,42 @@ def main():
         elapsed = float(t.item())
         torch.distributed.barrier()
 
-    corr_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_corr]))
-    look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look]))
+    gemm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_gemm]))
+    look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look])) / args.iters
     N = h8 * w8
     D = (2 * args.radius + 1) ** 2
     s = 2 if args.precision in ("bf16", "fp32-f16") else 4
+    levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
+    # algorithmic bytes
     look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
+    op_bytes = 2 if args.precision.startswith("bf16") else 4
+    gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
     gemm_flop = 2.0 * B * N * N * args.channels
-    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     compute_dt = "fp32" if args.precision.startswith("fp32") else "bf16"
-    corr_tfs = gemm_flop / (corr_ms * 1e-3) / 1e12
+    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+    gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
+    gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_lookup.json")
-    if os.path.exists(pmc):
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if os.path.exists(pmc_path):
         try:
-            with open(pmc) as fh:
-                traffic = json.load(fh).get(args.precision, {}).get("hbm_bytes_per_launch")
+            with open(pmc_path) as fh:
+                pmc = json.load(fh).get(args.precision, {})
         except (OSError, ValueError):
-            traffic = None
+            pmc = {}
+    roof_gemm = {"kernel": "corr_pyramid_stationary (MFMA GEMM + fused pooled-pyramid epilogue)",
+                 "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
+                 "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
+                 "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[compute_dt],
+                 "mfma_frac": gemm_tfs / MFMA_PEAK[compute_dt], "algorithmic_flop_per_launch": gemm_flop}
+    roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
+                 "traffic": pmc.get("lookup_hbm_bytes_per_launch"),
+                 "algorithmic_bytes_per_launch": look_bytes, "avg_launch_ms": look_ms,
+                 "launches_per_step": args.iters}
+    dominant_gemm = gemm_ms >= look_ms * args.iters
 
     if rank != 0:
         if world > 1:
@@ -206,14 +217,9 @@ def main():
                    "channels": args.channels, "batch_per_gpu": B, "global_batch": B * world,
                    "lookups_per_step": args.iters, "precision": args.precision,
                    "pyramid_storage": "fp16" if s == 2 else "fp32", "parallelism": f"batch-shard x{world}"},
-        "roofline": {"kernel": "rmd corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": look_bytes,
-                     "avg_launch_ms": look_ms, "launches_per_step": args.iters},
-        "roofline_corr": {"kernel": "rmd corr_pyramid (prep x2 + MFMA GEMM with pooled-pyramid epilogue)",
-                          "bound": "mfma", "achieved": corr_tfs, "peak": MFMA_PEAK[compute_dt],
-                          "unit": "TFLOP/s", "frac": corr_tfs / MFMA_PEAK[compute_dt],
-                          "algorithmic_flop_per_launch": gemm_flop, "avg_launch_ms": corr_ms},
+        "roofline": roof_gemm if dominant_gemm else roof_look,
+        "roofline_gemm": roof_gemm,
+        "roofline_lookup": roof_look,
     }
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args, h8, w8)

@@ -87,6 +87,14 @@ int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels,
                      const rmd_pyramid_desc* desc, int compute, void* pyramid, void* workspace,
                      void* stream);
 
+/* The two halves of rmd_corr_pyramid, for callers that time or overlap them separately:
+ * rmd_corr_prepare transposes/converts both feature maps into the workspace (pixel-major,
+ * channel-contiguous operands); rmd_corr_pyramid_prepared runs the GEMM + pyramid epilogue on them. */
+int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* desc,
+                     int compute, void* workspace, void* stream);
+int rmd_corr_pyramid_prepared(int channels, const rmd_pyramid_desc* desc, int compute, void* pyramid,
+                              void* workspace, void* stream);
+
 /*
  * Windowed bilinear pyramid lookup.  Replaces raft.CorrBlock.__call__ (raft.py:49-95):
  * level i is sampled at (x/2^i + a - r, y/2^i + b - r), bilinear, align_corners=True, zero

@@ -15,7 +15,7 @@
 // Two kernels:
 //  * corr_pyramid_stationary — performance path (bf16 operands, fp16 pyramid, C = 256): a
 //    16x16 target block's A operand stays in LDS while 4 waves (one per SIMD, 512-register
-//    budget) sweep 32-query tiles with B fragments software-pipelined one tile ahead.
+//    budget) sweep 32-query tiles; the next tile's B fragments load during the epilogue.
 //  * corr_pyramid_tiled — general path (exact f32 MFMA for parity, any C, f32 or fp16 storage):
 //    64 queries x 256 targets per workgroup, K staged through LDS in 64-deep chunks.
 // Operands are first transposed to pixel-major, channel-contiguous (B, N, Cp) by prep_operand.
@@ -51,14 +51,14 @@ __device__ __forceinline__ size_t lvl_index(const PyrGeom& g, int l, int b, int 
 // prep: (B, C, N) f32 -> (B, N, Cp) operand type, zero-padded channels.  64 px x 64 ch per block.
 template <typename T>
 __global__ void __launch_bounds__(kThreads)
-prep_operand(const float* __restrict__ f, T* __restrict__ o, int C, int N, int Cp) {
+prep_operand(const float* __restrict__ f, T* __restrict__ o, int C, int N, int Cp, float scale) {
     __shared__ float tile[64][65];
     const int b = blockIdx.z, p0 = blockIdx.x * 64, c0 = blockIdx.y * 64, t = threadIdx.x;
     const float* fb = f + (size_t)b * C * N;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int c = c0 + (t >> 6) + 4 * i, p = p0 + (t & 63);
-        tile[(t >> 6) + 4 * i][t & 63] = (c < C && p < N) ? fb[(size_t)c * N + p] : 0.f;
+        tile[(t >> 6) + 4 * i][t & 63] = (c < C && p < N) ? fb[(size_t)c * N + p] * scale : 0.f;
     }
     __syncthreads();
     const int p = p0 + (t >> 2);
@@ -255,9 +255,15 @@ corr_pyramid_tiled(const typename Operand<F32>::T* __restrict__ opA,   // fmap2 
 // 8 MFMA 32x32x16 tiles per k-step (all 256 targets x 32 queries), then pools in-lane and stores
 // every level straight from registers.  v_permlane32_swap pairs the two half-waves' 8-byte row
 // halves into full 16-byte row chunks, so one store instruction writes two contiguous 512-byte runs.
-constexpr int kSThreads = 256;
-constexpr int kSWaves = kSThreads / 64;
-constexpr int kStoresPerTile = 23;    // 16 (L0) + 4 (L1) + 2 (L2) + 1 (L3) per lane per 32-query tile
+// TH = 16-row halves per wave: TH = 2 -> 4 waves (one per SIMD) each own all 16 target rows;
+// TH = 1 -> 8 waves (two per SIMD) each own 8 rows, pairs of waves share a query tile.
+template <int TH> struct STraits {
+    static constexpr int kWaves = TH == 2 ? 4 : 8;
+    static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kTiles = 4 * TH;                 // MFMA 32x32 tiles per wave
+    static constexpr int kRows = 8 * TH;                  // level-0 target rows per wave
+    static constexpr int kStores = TH == 2 ? 23 : 12;     // stores per lane per 32-query tile
+};
 
 __device__ __forceinline__ unsigned pack_half2(float a, float b) {
     const __half2 h = __floats2half2_rn(a, b);
@@ -270,17 +276,23 @@ __device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
     y = r[1];
 }
 
+// per-wave store geometry: element offsets of the wave's first row/chunk on every level, row and
+// chunk strides, valid rows/chunks; a store address is base + uniform constant + per-lane offset
 struct SCtx {
-    int b, rb, cb, N;
-    float scale;
+    int N;
+    size_t base[4];     // level offset + row/chunk origin of this wave's rows (elements)
+    size_t rs[4];       // row stride (elements)
+    size_t cs[4];       // chunk stride = N * chunk width (elements)
+    int rows[4];        // valid rows of this wave per level
+    int chunks[4];      // valid chunks of this block per level (<= 2, 1, 1, 1)
 };
 
-// B-fragment loads in inline asm, retired by ONE hand-placed `s_waitcnt vmcnt(kStoresPerTile)`:
-// between a tile's loads and that wait the wave issues exactly kStoresPerTile compiler stores (the
-// epilogue, every store unconditional) and no other vector-memory op (no compiler-visible global
-// loads in the loop, no spills: checked in the .s by tests/test_asm_audit.py), so the wait retires
-// the loads while the previous tile's stores stay in flight.  hipcc does not count asm loads, so
-// it never inserts its own draining vmcnt(0).
+// B-fragment loads in inline asm, retired by ONE hand-placed `s_waitcnt vmcnt(kStores)`: between a
+// tile's loads and that wait the wave issues exactly kStores compiler stores (the epilogue, every
+// store unconditional) and no other vector-memory op (no compiler-visible global loads in the
+// loop, no spills: checked in the .s by tests/test_asm_audit.py), so the wait retires the loads
+// while the previous stores stay in flight.  hipcc does not count asm loads, so it never inserts
+// its own draining vmcnt(0).
 __device__ __forceinline__ void s_load_b_asm(bf16x8 (&bq)[16], const __bf16* src) {
 #define RMD_GLD(S) asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(bq[S]) : "v"(src), "i"((S) * 32) : "memory")
     RMD_GLD(0); RMD_GLD(1); RMD_GLD(2); RMD_GLD(3); RMD_GLD(4); RMD_GLD(5); RMD_GLD(6); RMD_GLD(7);
@@ -298,66 +310,83 @@ __device__ __forceinline__ void s_wait_b(bf16x8 (&bq)[16]) {
                  : "memory");
 }
 
-__device__ __forceinline__ void s_mma(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
-                                      const int (&arow)[8], int h) {
+template <int NT>
+__device__ __forceinline__ void s_lda(bf16x8 (&a)[NT], const unsigned char* smem, const int (&arow)[NT], int s, int h) {
     constexpr int Cp = 256, SWZ = 15;
 #pragma unroll
-    for (int ti = 0; ti < 8; ++ti)
+    for (int ti = 0; ti < NT; ++ti) {
+        const int row = arow[ti];
+        a[ti] = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * Cp * 2 + (((2 * s + h) ^ (row & SWZ)) << 4));
+    }
+}
+
+// 16 k-steps x NT MFMA tiles; the A fragments of step s+1 are read from LDS while step s's MFMAs run
+template <int NT>
+__device__ __forceinline__ void s_mma(f32x16 (&acc)[NT], const bf16x8 (&bq)[16], const unsigned char* smem,
+                                      const int (&arow)[NT], int h) {
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[ti][e] = 0.f;
+    bf16x8 a0[NT], a1[NT];
+    s_lda<NT>(a0, smem, arow, 0, h);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < 16; s += 2) {
+        s_lda<NT>(a1, smem, arow, s + 1, h);
 #pragma unroll
-        for (int ti = 0; ti < 8; ++ti) {
-            const int row = arow[ti];
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * Cp * 2 + (((2 * s + h) ^ (row & SWZ)) << 4));
-            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[s], acc[ti], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);   // bound the A-fragment look-ahead (register budget)
+        for (int ti = 0; ti < NT; ++ti) acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[ti], bq[s], acc[ti], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < 16) s_lda<NT>(a0, smem, arow, s + 2, h);
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[ti], bq[s + 1], acc[ti], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
 // Every store is unconditional: an invalid one (query past N, row or chunk outside a level, a
 // level beyond g.levels) is redirected to this lane's 16-B trash slot, so each tile issues exactly
-// kStoresPerTile stores (see s_load_b_asm).  ABL is a diagnostic ablation (RMD_ABLATE env):
-// 1 = every store to trash (no HBM write traffic).
+// kStores stores (see s_load_b_asm).  ABL is a diagnostic ablation (RMD_ABLATE env): 1 = every
+// store to trash (no HBM write traffic).
+// trash: this lane's slot in store-slot 0; slot k (a distinct 1 KiB line set per store of the
+// tile) keeps ABL = 1 stores from being merged by the compiler (the store count must stay exact)
 template <int ABL>
-__device__ __forceinline__ __half* sel(bool ok, __half* p, __half* trash) { return (ok && ABL != 1) ? p : trash; }
+__device__ __forceinline__ __half* sel(bool ok, __half* p, __half* trash, int k) {
+    if constexpr (ABL == 1) return trash + k * 64 * 8;
+    else return ok ? p : trash;
+}
 
-template <int ABL>
-__device__ __forceinline__ void s_epilogue(const f32x16 (&acc)[8], const SCtx& c, const PyrGeom& g, int q, int h,
+template <int TH, int ABL>
+__device__ __forceinline__ void s_epilogue(const f32x16 (&acc)[4 * TH], const SCtx& c, int q, int h,
                                            __half* __restrict__ pyr, __half* __restrict__ trash) {
+    constexpr int R0 = 8 * TH, R1 = 4 * TH, R2 = 2 * TH;
     const bool qv = q < c.N;
-    const int N = c.N, b = c.b, rb = c.rb, cb = c.cb;
-    const float scale = c.scale;
-    // V(row 0..15, cg 0..1, k 0..3) = level-0 value at target row, col 8cg + 4h + k
-#define V(row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)] * scale)
-    // level 0: rows 16rb + 8tr + 2m + h after the swap; chunk 2cb + tc
+    // per-lane parts of the addresses: query offset and the half-wave's row (h)
+    __half* p0 = pyr + c.base[0] + (size_t)q * 8 + h * c.rs[0];
+    __half* p1 = pyr + c.base[1] + (size_t)q * 8 + h * c.rs[1];
+    // V(row, cg 0..1, k 0..3) = level-0 value at the wave's target row, col 8cg + 4h + k (the
+    // 1/sqrt(C) scale is folded into the operands by prep_operand)
+#define V(row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)])
+    // level 0: rows 2m + h after the swap; chunk tc
 #pragma unroll
-    for (int tr = 0; tr < 2; ++tr) {
+    for (int tc = 0; tc < 2; ++tc) {
 #pragma unroll
-        for (int tc = 0; tc < 2; ++tc) {
-            const int xc = 2 * cb + tc;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int r0 = 8 * tr + 2 * m;
-                unsigned x0 = pack_half2(V(r0, tc, 0), V(r0, tc, 1));
-                unsigned x1 = pack_half2(V(r0, tc, 2), V(r0, tc, 3));
-                unsigned y0 = pack_half2(V(r0 + 1, tc, 0), V(r0 + 1, tc, 1));
-                unsigned y1 = pack_half2(V(r0 + 1, tc, 2), V(r0 + 1, tc, 3));
-                swap32(x0, y0);
-                swap32(x1, y1);
-                const int y = 16 * rb + r0 + h;
-                const bool ok = qv && y < g.ty[0] && xc < g.tx[0];
-                *reinterpret_cast<uint4*>(sel<ABL>(ok, pyr + lvl_index(g, 0, b, min(y, g.ty[0] - 1), xc, q, N), trash)) =
-                    make_uint4(x0, x1, y0, y1);
-            }
+        for (int m = 0; m < R0 / 2; ++m) {
+            const int r0 = 2 * m;
+            unsigned x0 = pack_half2(V(r0, tc, 0), V(r0, tc, 1));
+            unsigned x1 = pack_half2(V(r0, tc, 2), V(r0, tc, 3));
+            unsigned y0 = pack_half2(V(r0 + 1, tc, 0), V(r0 + 1, tc, 1));
+            unsigned y1 = pack_half2(V(r0 + 1, tc, 2), V(r0 + 1, tc, 3));
+            swap32(x0, y0);
+            swap32(x1, y1);
+            const bool ok = qv && r0 + h < c.rows[0] && tc < c.chunks[0];
+            *reinterpret_cast<uint4*>(sel<ABL>(ok, p0 + r0 * c.rs[0] + tc * c.cs[0], trash, tc * (R0 / 2) + m)) =
+                make_uint4(x0, x1, y0, y1);
         }
     }
-    // level 1: one 8x8 block; lane h holds cols {2h, 2h+1} (cg 0) and {4+2h, 5+2h} (cg 1)
-    float l1[8][2][2];
+    // level 1: lane h holds cols {2h, 2h+1} (cg 0) and {4+2h, 5+2h} (cg 1) of R1 rows
+    float l1[R1][2][2];
 #pragma unroll
-    for (int yy = 0; yy < 8; ++yy)
+    for (int yy = 0; yy < R1; ++yy)
 #pragma unroll
         for (int cg = 0; cg < 2; ++cg)
 #pragma unroll
@@ -365,69 +394,71 @@ __device__ __forceinline__ void s_epilogue(const f32x16 (&acc)[8], const SCtx& c
                 l1[yy][cg][u] = 0.25f * ((V(2 * yy, cg, 2 * u) + V(2 * yy, cg, 2 * u + 1)) +
                                          (V(2 * yy + 1, cg, 2 * u) + V(2 * yy + 1, cg, 2 * u + 1)));
 #undef V
-    const bool l1ok = qv && g.levels > 1 && cb < g.tx[1];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < R1 / 2; ++m) {
         unsigned x0 = pack_half2(l1[2 * m][0][0], l1[2 * m][0][1]);
         unsigned x1 = pack_half2(l1[2 * m][1][0], l1[2 * m][1][1]);
         unsigned y0 = pack_half2(l1[2 * m + 1][0][0], l1[2 * m + 1][0][1]);
         unsigned y1 = pack_half2(l1[2 * m + 1][1][0], l1[2 * m + 1][1][1]);
         swap32(x0, y0);
         swap32(x1, y1);
-        const int y = 8 * rb + 2 * m + h;
-        *reinterpret_cast<uint4*>(sel<ABL>(l1ok && y < g.ty[1], pyr + lvl_index(g, 1, b, min(y, g.ty[1] - 1), cb, q, N), trash)) =
-            make_uint4(x0, y0, x1, y1);
+        const bool ok = qv && 2 * m + h < c.rows[1] && c.chunks[1] > 0;
+        *reinterpret_cast<uint4*>(sel<ABL>(ok, p1 + 2 * m * c.rs[1], trash, R0 + m)) = make_uint4(x0, y0, x1, y1);
     }
-    // level 2: one 4x4 block; lane h holds cols {h, 2+h}; lane h stores rows 2h and 2h+1 (8 B each)
-    float l2[4][2];
+    // level 2: lane h holds cols {h, 2+h} of R2 rows; it stores rows (R2/2)h .. (R2/2)h + R2/2 - 1
+    float l2[R2][2];
 #pragma unroll
-    for (int yy = 0; yy < 4; ++yy)
+    for (int yy = 0; yy < R2; ++yy)
 #pragma unroll
         for (int cg = 0; cg < 2; ++cg)
             l2[yy][cg] = 0.25f * ((l1[2 * yy][cg][0] + l1[2 * yy][cg][1]) + (l1[2 * yy + 1][cg][0] + l1[2 * yy + 1][cg][1]));
     {
-        unsigned mine[4], other[4];
+        unsigned mine[R2], other[R2];
 #pragma unroll
-        for (int yy = 0; yy < 4; ++yy) {
+        for (int yy = 0; yy < R2; ++yy) {
             mine[yy] = pack_half2(l2[yy][0], l2[yy][1]);          // (col h, col 2+h)
             other[yy] = __shfl_xor(mine[yy], 32);
         }
-        const bool l2ok = qv && g.levels > 2 && cb < g.tx[2];
+        __half* p2 = pyr + c.base[2] + (size_t)q * 4 + (R2 / 2) * h * c.rs[2];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            // row 2h+k, selected with compile-time indices (a runtime index would go to scratch)
-            const unsigned mk = h ? mine[2 + k] : mine[k];
-            const unsigned ok_ = h ? other[2 + k] : other[k];
+        for (int k = 0; k < R2 / 2; ++k) {
+            // row (R2/2)h + k, selected with compile-time indices (a runtime index would go to scratch)
+            const unsigned mk = h ? mine[R2 / 2 + k] : mine[k];
+            const unsigned ok_ = h ? other[R2 / 2 + k] : other[k];
             const unsigned e0 = h ? ok_ : mk;      // cols 0 and 2 (held by h = 0)
             const unsigned e1 = h ? mk : ok_;      // cols 1 and 3 (held by h = 1)
-            const int y = 4 * rb + 2 * h + k;
-            *reinterpret_cast<uint2*>(sel<ABL>(l2ok && y < g.ty[2], pyr + lvl_index(g, 2, b, min(y, g.ty[2] - 1), cb, q, N), trash)) =
+            const bool ok = qv && (R2 / 2) * h + k < c.rows[2] && c.chunks[2] > 0;
+            *reinterpret_cast<uint2*>(sel<ABL>(ok, p2 + k * c.rs[2], trash, R0 + R1 / 2 + k)) =
                 make_uint2((e0 & 0xffffu) | (e1 << 16), (e0 >> 16) | (e1 & 0xffff0000u));
         }
     }
-    // level 3: one 2x2 block; lane h stores row h (4 B)
+    // level 3: TH rows of 2 cols; lane h stores row h (TH = 2) or both halves row 0 (TH = 1,
+    // identical values to the same address)
     {
-        float p3[2][2];
+        float t3[TH][2];
 #pragma unroll
-        for (int yy = 0; yy < 2; ++yy)
+        for (int yy = 0; yy < TH; ++yy)
 #pragma unroll
             for (int cg = 0; cg < 2; ++cg) {
                 const float s_ = l2[2 * yy][cg] + l2[2 * yy + 1][cg];
-                p3[yy][cg] = 0.25f * (s_ + __shfl_xor(s_, 32));
+                t3[yy][cg] = 0.25f * (s_ + __shfl_xor(s_, 32));
             }
-        const int y = 2 * rb + h;
-        const bool ok = qv && g.levels > 3 && cb < g.tx[3] && y < g.ty[3];
-        const unsigned v = h ? pack_half2(p3[1][0], p3[1][1]) : pack_half2(p3[0][0], p3[0][1]);
-        *reinterpret_cast<unsigned*>(sel<ABL>(ok, pyr + lvl_index(g, 3, b, min(y, g.ty[3] - 1), cb, q, N), trash)) = v;
+        const int yrow = TH == 2 ? h : 0;
+        unsigned v;
+        if constexpr (TH == 2) v = h ? pack_half2(t3[1][0], t3[1][1]) : pack_half2(t3[0][0], t3[0][1]);
+        else v = pack_half2(t3[0][0], t3[0][1]);
+        const bool ok = qv && yrow < c.rows[3] && c.chunks[3] > 0;
+        *reinterpret_cast<unsigned*>(sel<ABL>(ok, pyr + c.base[3] + (size_t)q * 2 + yrow * c.rs[3], trash, R0 + R1 / 2 + R2 / 2)) = v;
     }
 }
 
 // ABL (diagnostic, RMD_ABLATE env): 0 = normal, 1 = every store to trash, 2 = no MFMA
-template <int ABL>
-__global__ void __launch_bounds__(kSThreads, 1)
-corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, float scale, PyrGeom g,
-                        int qsplit, __half* __restrict__ pyr, __half* __restrict__ trash_base) {
-    constexpr int Cp = 256, CPR = Cp / 8, SWZ = 15;
+template <int TH, int ABL>
+__global__ void __launch_bounds__(STraits<TH>::kThreads, 1)
+corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
+                        __half* __restrict__ pyr, __half* __restrict__ trash_base) {
+    using Tr = STraits<TH>;
+    constexpr int Cp = 256, CPR = Cp / 8, SWZ = 15, NT = Tr::kTiles;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int H = g.height, W = g.width, N = H * W;
@@ -446,12 +477,15 @@ corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict
     const int ty0 = rb * 16, tx0 = cb * 16;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);    // wave-uniform: scalar loop control
+    const int th = TH == 2 ? 0 : (w & 1);                       // which 8-row half (TH = 1)
+    const int qslot = TH == 2 ? w : (w >> 1);                   // query-tile slot
+    constexpr int kSlots = TH == 2 ? Tr::kWaves : Tr::kWaves / 2;
     const int j = lane & 31, h = lane >> 5;
     __half* trash = trash_base + lane * 8;            // 16 B per lane (stores of all waves may collide)
 
     // ---- A block -> LDS (zero rows for targets outside the image) ------------------------------
     const __bf16* gA = opA + (size_t)b * N * Cp;
-    for (int id = tid; id < 256 * CPR; id += kSThreads) {
+    for (int id = tid; id < 256 * CPR; id += Tr::kThreads) {
         const int row = id / CPR, c = id - row * CPR;
         const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
         uint4 v = make_uint4(0, 0, 0, 0);
@@ -460,58 +494,75 @@ corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict
     }
     __syncthreads();
 
-    int arow[8];
+    // LDS row of this lane's A fragment for tile ti (4 target rows x 8 target cols)
+    int arow[NT];
 #pragma unroll
-    for (int ti = 0; ti < 8; ++ti) arow[ti] = (4 * (ti >> 1) + (j >> 3)) * 16 + 8 * (ti & 1) + (j & 7);
+    for (int ti = 0; ti < NT; ++ti) arow[ti] = (8 * th + 4 * (ti >> 1) + (j >> 3)) * 16 + 8 * (ti & 1) + (j & 7);
 
     SCtx c;
-    c.b = b; c.rb = rb; c.cb = cb; c.N = N; c.scale = scale;
+    c.N = N;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int cw = g.tw[l], span = (16 >> l) / (3 - TH), nch = l == 0 ? 2 : 1;   // rows of this wave
+        const int y0 = rb * (16 >> l) + th * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        c.cs[l] = (size_t)N * cw;
+        c.rs[l] = lv ? (size_t)g.tx[l] * N * cw : 0;
+        c.base[l] = lv ? (size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw : 0;
+        c.rows[l] = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        c.chunks[l] = lv ? max(0, min(nch, g.tx[l] - xc0)) : 0;
+    }
 
     const __bf16* gB = opB + (size_t)b * N * Cp;
     const int nqt = (N + 31) >> 5;
-    const int stride = kSWaves * qsplit;
-    int qt = split * kSWaves + w;
+    const int stride = kSlots * qsplit;
+    int qt = split * kSlots + qslot;
     if (qt >= nqt) return;
-    // software pipeline: tile t+1's B fragments load while tile t's MFMAs and epilogue run
-    bf16x8 b0[16], b1[16];
-    f32x16 acc[8];
+    // software pipeline: tile t+1's B fragments load right after tile t's MFMAs (their registers
+    // are free then) and land while tile t's epilogue runs; one B buffer, one explicit wait
+    bf16x8 bq[16];
+    f32x16 acc[NT];
     const int last = nqt - 1;
     const size_t hoff = 8 * h;
-    s_load_b_asm(b0, gB + (size_t)min(qt * 32 + j, N - 1) * Cp + hoff);
-    s_wait_b<0>(b0);
+    s_load_b_asm(bq, gB + (size_t)min(qt * 32 + j, N - 1) * Cp + hoff);
+    s_wait_b<0>(bq);
     while (true) {
         const int qn = qt + stride;
-        s_load_b_asm(b1, gB + (size_t)min(min(qn, last) * 32 + j, N - 1) * Cp + hoff);
-        if constexpr (ABL != 2) s_mma(acc, b0, smem, arow, h);
-        else for (int ti = 0; ti < 8; ++ti) for (int e = 0; e < 16; ++e) acc[ti][e] = b0[0][0] * 0.f;
-        s_epilogue<ABL>(acc, c, g, qt * 32 + j, h, pyr, trash);
-        s_wait_b<kStoresPerTile>(b1);
+        if constexpr (ABL != 2) s_mma<NT>(acc, bq, smem, arow, h);
+        else for (int ti = 0; ti < NT; ++ti) for (int e = 0; e < 16; ++e) acc[ti][e] = bq[0][0] * 0.f;
+        s_load_b_asm(bq, gB + (size_t)min(min(qn, last) * 32 + j, N - 1) * Cp + hoff);
+        s_epilogue<TH, ABL>(acc, c, qt * 32 + j, h, pyr, trash);
+        s_wait_b<Tr::kStores>(bq);
         if (qn >= nqt) break;
-        const int qn2 = qn + stride;
-        s_load_b_asm(b0, gB + (size_t)min(min(qn2, last) * 32 + j, N - 1) * Cp + hoff);
-        if constexpr (ABL != 2) s_mma(acc, b1, smem, arow, h);
-        else for (int ti = 0; ti < 8; ++ti) for (int e = 0; e < 16; ++e) acc[ti][e] = b1[0][0] * 0.f;
-        s_epilogue<ABL>(acc, c, g, qn * 32 + j, h, pyr, trash);
-        s_wait_b<kStoresPerTile>(b0);
-        if (qn2 >= nqt) break;
-        qt = qn2;
+        qt = qn;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool F32, typename TOut>
-int launch_pyramid(const float* f1, const float* f2, int C, const rmd_pyramid_desc& d, void* pyramid,
-                   void* workspace, hipStream_t st) {
+template <bool F32>
+int launch_prepare(const float* f1, const float* f2, int C, const rmd_pyramid_desc& d, void* workspace,
+                   hipStream_t st) {
     using T = typename Operand<F32>::T;
     const int N = d.height * d.width;
     const int Cp = (C + kKC - 1) / kKC * kKC;
     T* opA = reinterpret_cast<T*>(workspace);
     T* opB = opA + (size_t)d.batch * N * Cp;
     dim3 pg((N + 63) / 64, Cp / 64, d.batch);
-    prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp);
-    prep_operand<T><<<pg, kThreads, 0, st>>>(f1, opB, C, N, Cp);
-    int rc = check_launch("rmd_corr_pyramid/prep");
-    if (rc) return rc;
+    // bf16 perf path: the 1/sqrt(C) scale is folded into fmap2 before rounding (exact for C = 4^k,
+    // e.g. the reference's 256); the f32 parity path scales the f32 accumulators in the epilogue
+    const float prescale = F32 ? 1.0f : 1.0f / sqrtf((float)C);
+    prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp, prescale);
+    prep_operand<T><<<pg, kThreads, 0, st>>>(f1, opB, C, N, Cp, 1.0f);
+    return check_launch("rmd_corr_prepare");
+}
+
+template <bool F32, typename TOut>
+int launch_pyramid(int C, const rmd_pyramid_desc& d, void* pyramid, void* workspace, hipStream_t st) {
+    using T = typename Operand<F32>::T;
+    const int N = d.height * d.width;
+    const int Cp = (C + kKC - 1) / kKC * kKC;
+    T* opA = reinterpret_cast<T*>(workspace);
+    T* opB = opA + (size_t)d.batch * N * Cp;
     const float scale = 1.0f / sqrtf((float)C);
     const PyrGeom geom = make_geom(d);
     if constexpr (!F32 && sizeof(TOut) == 2) {
@@ -519,22 +570,23 @@ int launch_pyramid(const float* f1, const float* f2, int C, const rmd_pyramid_de
             const int nblk = ((d.height + 15) / 16) * ((d.width + 15) / 16);
             const int nqt = (N + 31) / 32;
             int qsplit = 1;
-            while (nblk * d.batch * qsplit < 256 && qsplit * kSWaves * 4 <= nqt) qsplit *= 2;
+            while (nblk * d.batch * qsplit < 256 && qsplit * 16 <= nqt) qsplit *= 2;
             const int lds = 256 * Cp * 2;
             const int nwg = nblk * d.batch * qsplit;
             __half* out = reinterpret_cast<__half*>(pyramid);
             __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * N * Cp);
             const char* abl_env = getenv("RMD_ABLATE");
             const int abl = abl_env ? atoi(abl_env) : 0;
-            switch (abl) {
-#define RMD_SCASE(ABL)                                                                                          \
-    case ABL:                                                                                                   \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<ABL>),                  \
+            const char* w_env = getenv("RMD_GEMM_WAVES");           // 4 (default) or 8
+            const int th = (w_env && atoi(w_env) == 8) ? 1 : 2;
+            switch (th * 4 + (abl >= 0 && abl <= 2 ? abl : 0)) {
+#define RMD_SCASE(TH, ABL)                                                                                      \
+    case TH * 4 + ABL:                                                                                          \
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<TH, ABL>),              \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);                             \
-        corr_pyramid_stationary<ABL><<<nwg, kSThreads, lds, st>>>(opA, opB, scale, geom, qsplit, out, trash);   \
+        corr_pyramid_stationary<TH, ABL><<<nwg, STraits<TH>::kThreads, lds, st>>>(opA, opB, geom, qsplit, out, trash); \
         break;
-                RMD_SCASE(1) RMD_SCASE(2)
-                default: RMD_SCASE(0)
+                RMD_SCASE(1, 0) RMD_SCASE(1, 1) RMD_SCASE(1, 2) RMD_SCASE(2, 0) RMD_SCASE(2, 1) RMD_SCASE(2, 2)
 #undef RMD_SCASE
             }
             return check_launch("rmd_corr_pyramid/gemm-stationary");
@@ -544,8 +596,17 @@ int launch_pyramid(const float* f1, const float* f2, int C, const rmd_pyramid_de
     auto kern = corr_pyramid_tiled<F32, TOut>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     dim3 grid((N + kBQ - 1) / kBQ, ((d.height + 15) / 16) * ((d.width + 15) / 16), d.batch);
-    kern<<<grid, kThreads, lds, st>>>(opA, opB, Cp, scale, geom, reinterpret_cast<TOut*>(pyramid));
+    kern<<<grid, kThreads, lds, st>>>(opA, opB, Cp, F32 ? scale : 1.0f, geom, reinterpret_cast<TOut*>(pyramid));
     return check_launch("rmd_corr_pyramid/gemm");
+}
+
+int check_args(const rmd_pyramid_desc* d, int channels, int compute) {
+    RMD_REQUIRE(d, RMD_ERR_ARG, "rmd_corr_pyramid: null desc");
+    RMD_REQUIRE(channels > 0, RMD_ERR_SHAPE, "rmd_corr_pyramid: channels must be > 0");
+    RMD_REQUIRE(d->levels >= 1 && d->levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_pyramid: bad levels");
+    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16, RMD_ERR_ARG, "rmd_corr_pyramid: compute must be F32 or BF16");
+    RMD_REQUIRE(d->storage == RMD_F32 || d->storage == RMD_F16, RMD_ERR_ARG, "rmd_corr_pyramid: storage must be F32 or F16");
+    return RMD_OK;
 }
 
 }  // namespace
@@ -555,23 +616,35 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     if (!d || channels <= 0) return 0;
     const size_t Cp = (size_t)(channels + rmd::kKC - 1) / rmd::kKC * rmd::kKC;
     const size_t es = compute == RMD_F32 ? 4 : 2;
-    return 2 * (size_t)d->batch * d->height * d->width * Cp * es + 1024;   // + 64 lanes x 16 B trash
+    return 2 * (size_t)d->batch * d->height * d->width * Cp * es + 32 * 1024;   // + trash slots (<= 32 x 1 KiB)
+}
+
+extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,
+                                int compute, void* workspace, void* stream) {
+    RMD_REQUIRE(fmap1 && fmap2 && workspace, RMD_ERR_ARG, "rmd_corr_prepare: null pointer");
+    int rc = rmd::check_args(d, channels, compute);
+    if (rc) return rc;
+    hipStream_t st = rmd::as_stream(stream);
+    return compute == RMD_BF16 ? rmd::launch_prepare<false>(fmap1, fmap2, channels, *d, workspace, st)
+                               : rmd::launch_prepare<true>(fmap1, fmap2, channels, *d, workspace, st);
+}
+
+extern "C" int rmd_corr_pyramid_prepared(int channels, const rmd_pyramid_desc* d, int compute, void* pyramid,
+                                         void* workspace, void* stream) {
+    RMD_REQUIRE(pyramid && workspace, RMD_ERR_ARG, "rmd_corr_pyramid_prepared: null pointer");
+    int rc = rmd::check_args(d, channels, compute);
+    if (rc) return rc;
+    hipStream_t st = rmd::as_stream(stream);
+    if (compute == RMD_BF16)
+        return d->storage == RMD_F16 ? rmd::launch_pyramid<false, __half>(channels, *d, pyramid, workspace, st)
+                                     : rmd::launch_pyramid<false, float>(channels, *d, pyramid, workspace, st);
+    return d->storage == RMD_F16 ? rmd::launch_pyramid<true, __half>(channels, *d, pyramid, workspace, st)
+                                 : rmd::launch_pyramid<true, float>(channels, *d, pyramid, workspace, st);
 }
 
 extern "C" int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,
                                 int compute, void* pyramid, void* workspace, void* stream) {
-    RMD_REQUIRE(fmap1 && fmap2 && d && pyramid && workspace, RMD_ERR_ARG, "rmd_corr_pyramid: null pointer");
-    RMD_REQUIRE(channels > 0, RMD_ERR_SHAPE, "rmd_corr_pyramid: channels must be > 0");
-    RMD_REQUIRE(d->levels >= 1 && d->levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_pyramid: bad levels");
-    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16, RMD_ERR_ARG, "rmd_corr_pyramid: compute must be F32 or BF16");
-    hipStream_t st = rmd::as_stream(stream);
-    if (compute == RMD_BF16) {
-        if (d->storage == RMD_F16) return rmd::launch_pyramid<false, __half>(fmap1, fmap2, channels, *d, pyramid, workspace, st);
-        if (d->storage == RMD_F32) return rmd::launch_pyramid<false, float>(fmap1, fmap2, channels, *d, pyramid, workspace, st);
-    } else {
-        if (d->storage == RMD_F16) return rmd::launch_pyramid<true, __half>(fmap1, fmap2, channels, *d, pyramid, workspace, st);
-        if (d->storage == RMD_F32) return rmd::launch_pyramid<true, float>(fmap1, fmap2, channels, *d, pyramid, workspace, st);
-    }
-    rmd::set_error("rmd_corr_pyramid: storage must be F32 or F16");
-    return RMD_ERR_ARG;
+    int rc = rmd_corr_prepare(fmap1, fmap2, channels, d, compute, workspace, stream);
+    if (rc) return rc;
+    return rmd_corr_pyramid_prepared(channels, d, compute, pyramid, workspace, stream);
 }

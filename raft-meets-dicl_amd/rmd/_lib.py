@@ -46,6 +46,8 @@ _SIGS = {
     "rmd_corr_pyramid_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PyramidDesc), _I, _I]),
     "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_lookup": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
+    "rmd_corr_prepare": (_I, [_P, _P, _I, ctypes.POINTER(PyramidDesc), _I, _P, _P]),
+    "rmd_corr_pyramid_prepared": (_I, [_I, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_dicl_stack": (_I, [_P, _P, _P] + [_I] * 11 + [_P, _P]),
     "rmd_dicl_stack_backward": (_I, [_P, _P] + [_I] * 11 + [_P, _P, _P]),
     "rmd_dicl_stack_int_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I]),

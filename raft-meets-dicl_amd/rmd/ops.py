@@ -73,8 +73,12 @@ class Pyramid:
         return x.float().reshape(b, h, w, 1, hl, wl)
 
 
-def corr_pyramid(fmap1, fmap2, levels=4, precision=None):
-    """raft.CorrBlock.__init__ (raft.py:18-47) on the GPU -> Pyramid."""
+def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None):
+    """raft.CorrBlock.__init__ (raft.py:18-47) on the GPU -> Pyramid.
+
+    ``events`` (optional list) receives (start, end) HIP events bracketing the GEMM launch alone
+    (the operand prep runs before the start event) — bench.py's roofline timing.
+    """
     _require_gpu(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
@@ -88,8 +92,17 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None):
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=f1.device)
     data = torch.empty(d.total_elements, dtype=_STORAGE_DTYPE[storage], device=f1.device)
     with torch.cuda.device(f1.device):
-        _lib.check(lib.rmd_corr_pyramid(_ptr(f1), _ptr(f2), c, ctypes.byref(d), compute, _ptr(data), _ptr(ws),
-                                        _lib.stream_ptr(f1.device)), "rmd_corr_pyramid")
+        stream = _lib.stream_ptr(f1.device)
+        _lib.check(lib.rmd_corr_prepare(_ptr(f1), _ptr(f2), c, ctypes.byref(d), compute, _ptr(ws), stream),
+                   "rmd_corr_prepare")
+        if events is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.check(lib.rmd_corr_pyramid_prepared(c, ctypes.byref(d), compute, _ptr(data), _ptr(ws), stream),
+                   "rmd_corr_pyramid_prepared")
+        if events is not None:
+            e1.record()
+            events.append((e0, e1))
     return Pyramid(data, d, c)
 
 
@@ -208,7 +221,9 @@ class _Dap(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
         _require_gpu(x, weight)
-        b, dd = x.shape[:2]
+        b, dd = x.shape[0], weight.shape[0]
+        if x.numel() % (b * dd) or weight.numel() != dd * dd:
+            raise ValueError(f"dap: x {tuple(x.shape)} does not hold {dd} displacement channels per batch")
         xc = x.detach().float().contiguous()
         wc = weight.detach().float().reshape(dd, dd).contiguous()
         n = xc.numel() // (b * dd)
@@ -222,7 +237,7 @@ class _Dap(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         xc, wc = ctx.saved_tensors
-        b, dd = xc.shape[:2]
+        b, dd = xc.shape[0], wc.shape[0]
         n = xc.numel() // (b * dd)
         g = grad.float().contiguous()
         gx = None

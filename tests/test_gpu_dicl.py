@@ -104,7 +104,10 @@ def test_dicl_compute_cost_golden():
     g = load_golden("dicl_cost_b2_c16_10x12")
     mnet = rmd.blocks.dicl.MatchingNet(32)
     assert sorted(mnet.state_dict().keys()) == sorted(g["sd.keys"].tolist())
-    mnet = det_init(mnet).to(DEV).eval()
+    holder = torch.nn.Module()
+    holder.mnet = mnet                      # det_init keys as inside FlowLevel: 'mnet.0.0.weight', ...
+    det_init(holder)
+    mnet = mnet.to(DEV).eval()
     with torch.no_grad():
         cost = rmd.dicl.compute_cost(mnet, _t(g["fmap1"]), _t(g["fmap2"]), g["maxdisp"].tolist())
     assert rel_max_err(cost.cpu().numpy(), g["cost"]) < 1e-4

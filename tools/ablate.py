@@ -49,10 +49,17 @@ def main():
     res["copy_0.55GB_TBps"] = 2 * src.numel() * 4 / t / 1e9
     del big, src, dst
     f1, f2, coords = bench.synthetic(8, 256, 55, 128, 12, 1234, dev)
-    for abl in (0, 1, 2):
-        os.environ["RMD_ABLATE"] = str(abl)
-        res[f"corr_pyramid_abl{abl}_ms"] = timeit(lambda: ops.corr_pyramid(f1, f2, 4, "bf16"))
+    for waves in ("8", "4"):
+        os.environ["RMD_GEMM_WAVES"] = waves
+        for abl in (0, 1, 2):
+            os.environ["RMD_ABLATE"] = str(abl)
+            res[f"corr_pyramid_w{waves}_abl{abl}_ms"] = timeit(lambda: ops.corr_pyramid(f1, f2, 4, "bf16"))
     os.environ["RMD_ABLATE"] = "0"
+    os.environ.pop("RMD_GEMM_WAVES")
+    os.environ["RMD_FORCE_TILED_GEMM"] = "1"
+    res["corr_pyramid_tiled_bf16_ms"] = timeit(lambda: ops.corr_pyramid(f1, f2, 4, "bf16"))
+    os.environ.pop("RMD_FORCE_TILED_GEMM")
+    res["corr_pyramid_fp32_ms"] = timeit(lambda: ops.corr_pyramid(f1, f2, 4, "fp32"), reps=3, warm=1)
     pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
     for abl in (0, 1, 2):
         os.environ["RMD_ABLATE"] = str(abl)
