@@ -106,6 +106,37 @@ int rmd_corr_lookup(const void* pyramid, const rmd_pyramid_desc* desc, const flo
                     int radius, unsigned zero_level_mask, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Backward of the RAFT correlation (training; autograd of raft.py:18-95).  Coordinates are
+ * detached in the reference (raft.py:402), so only the feature maps receive gradients.
+ *
+ * Gradient of the pyramid, dense float32 "G": (B, N, T) row-major with T = rmd_corr_grad_targets()
+ * = sum_l H_l*W_l; level l of query row (b, p) occupies columns [t_off(l), t_off(l) + H_l*W_l) with
+ * t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at t_off(l) + y*W_l + x.  With
+ * P = rmd_corr_pool_targets(fmap2, scale = 1/sqrt(C)) as (B, T, C):
+ *   grad_fmap1 (B, C, N) = P^T G^T    and    dP (B, T, C) = G^T fmap1^T      (plain GEMMs)
+ *   grad_fmap2 = rmd_corr_unpool_targets(dP, scale = 1/sqrt(C)).
+ */
+
+/* Targets per query row of G (all levels), or -1 on bad sizes.  Host-only. */
+long long rmd_corr_grad_targets(int height, int width, int levels);
+
+/* grad_levels (G, caller-zeroed once per forward) += d(lookup)/d(pyramid)^T grad_out, where
+ * grad_out is (B, L*(2r+1)^2, H, W) like rmd_corr_lookup's output.  Replaces the
+ * grid_sampler_2d_backward of raft.py:80.  Zeroed levels (mask) and 1-pixel (NaN) levels add
+ * nothing.  Deterministic (no atomics). */
+int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* desc, const float* coords,
+                             int radius, unsigned zero_level_mask, float* grad_levels, void* stream);
+
+/* pooled (B, T, C) = avg_pool_{2^l}(fmap2) * scale for every level (raft.py:35-47 applied to the
+ * feature map, which commutes with the product). */
+int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,
+                          float scale, float* pooled, void* stream);
+
+/* grad_fmap2 (B, C, H, W) = scale * sum_l avg_pool_{2^l}^T(grad_pooled level l)  (avg_pool2d_backward). */
+int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
+                            float scale, float* grad_fmap2, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);
  * stack (B, d, d, 2C [+2], h, w) float32 contiguous with d = 2r+1, dim 1 the x-offset a-r and
  * dim 2 the y-offset b-r — exactly the MatchingNet input (blocks/dicl.py:111-118).  h*w must be a

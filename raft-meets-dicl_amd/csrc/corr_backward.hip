@@ -1,0 +1,221 @@
+// corr_backward.hip — gradients of the RAFT correlation pyramid and its windowed lookup.
+//
+// Replaces the autograd of raft.CorrBlock (qzed/raft-meets-dicl src/models/impls/raft.py:18-95):
+// grid_sampler_2d_backward of the lookup (:80; coordinates are detached at raft.py:402, so only the
+// volume receives a gradient), avg_pool2d_backward of the pyramid (:45) and the bmm transposes of
+// the all-pairs product (:30-33).
+//
+// Decomposition (backward):
+//   level l of the pyramid equals fmap1 . P_l with P_l = avg-pooled fmap2 / sqrt(C) (the pooling
+//   commutes with the product), so with G_l = dL/d(level l):
+//     dfmap1[p]  = sum_l sum_t G_l[p, t] P_l[t]                         (GEMM, K = sum_l T_l)
+//     dP_l[t]    = sum_p G_l[p, t] fmap1[p]                              (GEMM, K = N)
+//     dfmap2     = sum_l unpool_l(dP_l) / sqrt(C)                        (this file)
+//   G (all levels, all lookups of a forward) is accumulated densely as (B, N, T) float32,
+//   T = sum_l H_l W_l, level l's targets at column offset t_off[l] = sum_{l'<l} H_l' W_l', row-major
+//   (y, x) inside a level — a plain strided matrix, so both GEMMs are library GEMMs.
+//   rmd_corr_lookup_backward: one lane per (query, level) owns row (b, p) of level l: it spreads
+//   the (2r+1)^2 tap gradients over its (2r+2)^2 integer patch with the forward's bilinear
+//   weights (separable: x then y) and read-modify-writes the patch — no atomics, no other lane
+//   touches that row in the launch, and successive lookups are ordered by the stream.
+
+#include "rmd_common.h"
+
+namespace rmd {
+namespace {
+
+constexpr int kThreads = 256;
+
+__host__ __device__ inline long long level_targets(int h, int w, int l) { return (long long)(h >> l) * (w >> l); }
+
+struct GradGeom {
+    int batch, height, width, levels;
+    int lh[RMD_MAX_LEVELS], lw[RMD_MAX_LEVELS];
+    long long toff[RMD_MAX_LEVELS];   // column offset of level l inside a query row
+    long long T;                      // targets per query row (all levels)
+};
+
+inline GradGeom make_grad_geom(int batch, int h, int w, int levels) {
+    GradGeom g{};
+    g.batch = batch;
+    g.height = h;
+    g.width = w;
+    g.levels = levels;
+    long long t = 0;
+    for (int l = 0; l < levels; ++l) {
+        g.lh[l] = h >> l;
+        g.lw[l] = w >> l;
+        g.toff[l] = t;
+        t += (long long)g.lh[l] * g.lw[l];
+    }
+    g.T = t;
+    return g;
+}
+
+// grid: (query blocks, batch, level); one lane per (query, level)
+template <int R>
+__global__ void __launch_bounds__(kThreads)
+corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const float* __restrict__ coords,
+                            unsigned zmask, float* __restrict__ grad) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    const int N = g.height * g.width;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int b = blockIdx.y, L = blockIdx.z;
+    if (p >= N) return;
+    if ((zmask >> L) & 1u) return;                       // zeroed level (raft.py:86-87): no gradient
+    const int lh = g.lh[L], lw = g.lw[L];
+    if (lh < 2 || lw < 2) return;                        // NaN level of the reference: no gradient
+    const float inv = 1.0f / (float)(1 << L);
+    float cx = coords[((size_t)b * 2 + 0) * N + p] * inv;
+    float cy = coords[((size_t)b * 2 + 1) * N + p] * inv;
+    cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+    cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+    const float fx0 = floorf(cx), fy0 = floorf(cy);
+    const float fx = cx - fx0, fy = cy - fy0;
+    const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+
+    const float* go = gout + ((size_t)b * g.levels + L) * D * D * (size_t)N + p;
+    float* row = grad + ((size_t)b * N + p) * g.T + g.toff[L];
+
+    // x pass per tap row bb: Q[bb][i] = g[i][bb](1-fx) + g[i-1][bb] fx, i = 0..K-1
+    // y pass: P[j][i] = Q[j][i](1-fy) + Q[j-1][i] fy; rows j of the patch are written as produced
+    float qprev[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) qprev[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        float qcur[K];
+        if (j < D) {
+            float gr[D];
+#pragma unroll
+            for (int a = 0; a < D; ++a) gr[a] = go[(size_t)(a * D + j) * N];   // channel a*D + bb, bb = j
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                qcur[i] = (i < D ? gr[i] * (1.0f - fx) : 0.f) + (i >= 1 ? gr[i - 1] * fx : 0.f);
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) qcur[i] = 0.f;
+        }
+        const int y = ys + j;
+        if (y >= 0 && y < lh) {
+            float* r = row + (size_t)y * lw;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int x = xs + i;
+                if (x >= 0 && x < lw) r[x] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) qprev[i] = qcur[i];
+    }
+}
+
+// P (B, T, C) = avg-pooled fmap2 / sqrt(C), all levels; one thread per (b, t, c), c fastest
+__global__ void __launch_bounds__(kThreads)
+pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, float scale, float* __restrict__ P) {
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const long long total = (long long)g.batch * g.T * C;
+    if (idx >= total) return;
+    const int c = (int)(idx % C);
+    const long long bt = idx / C;
+    const long long t = bt % g.T;
+    const int b = (int)(bt / g.T);
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < RMD_MAX_LEVELS; ++k)
+        if (k < g.levels && t >= g.toff[k]) l = k;
+    const int tl = (int)(t - g.toff[l]);
+    const int y = tl / g.lw[l], x = tl - y * g.lw[l];
+    const int s = 1 << l;
+    const float* src = f + ((size_t)b * C + c) * g.height * g.width + (size_t)(y * s) * g.width + x * s;
+    float acc = 0.f;
+    for (int dy = 0; dy < s; ++dy)
+        for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.width + dx];
+    P[idx] = acc * (scale / (float)(s * s));
+}
+
+// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l; one thread per output element
+__global__ void __launch_bounds__(kThreads)
+unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float scale, float* __restrict__ df) {
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int HW = g.height * g.width;
+    const long long total = (long long)g.batch * C * HW;
+    if (idx >= total) return;
+    const int px = (int)(idx % HW);
+    const long long bc = idx / HW;
+    const int c = (int)(bc % C), b = (int)(bc / C);
+    const int y = px / g.width, x = px - y * g.width;
+    const float* base = dP + (size_t)b * g.T * C + c;
+    float acc = 0.f;
+#pragma unroll
+    for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
+        if (l >= g.levels) break;
+        const int yl = y >> l, xl = x >> l;
+        if (yl < g.lh[l] && xl < g.lw[l])
+            acc += base[(size_t)(g.toff[l] + (long long)yl * g.lw[l] + xl) * C] * (1.0f / (float)(1 << (2 * l)));
+    }
+    df[idx] = acc * scale;
+}
+
+int check_grad_args(int batch, int channels, int h, int w, int levels) {
+    RMD_REQUIRE(batch >= 1 && channels >= 1 && h >= 1 && w >= 1, RMD_ERR_SHAPE, "rmd corr backward: bad sizes");
+    RMD_REQUIRE(levels >= 1 && levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd corr backward: bad levels");
+    RMD_REQUIRE((h >> (levels - 1)) >= 1 && (w >> (levels - 1)) >= 1, RMD_ERR_SHAPE,
+                "rmd corr backward: level %d of a %dx%d map is empty", levels - 1, h, w);
+    return RMD_OK;
+}
+
+}  // namespace
+}  // namespace rmd
+
+extern "C" long long rmd_corr_grad_targets(int height, int width, int levels) {
+    if (height < 1 || width < 1 || levels < 1 || levels > RMD_MAX_LEVELS) return -1;
+    long long t = 0;
+    for (int l = 0; l < levels; ++l) t += rmd::level_targets(height, width, l);
+    return t;
+}
+
+extern "C" int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* d, const float* coords,
+                                        int radius, unsigned zero_level_mask, float* grad_levels, void* stream) {
+    RMD_REQUIRE(grad_out && d && coords && grad_levels, RMD_ERR_ARG, "rmd_corr_lookup_backward: null pointer");
+    int rc = rmd::check_grad_args(d->batch, 1, d->height, d->width, d->levels);
+    if (rc) return rc;
+    const rmd::GradGeom g = rmd::make_grad_geom(d->batch, d->height, d->width, d->levels);
+    const int N = d->height * d->width;
+    dim3 grid((N + rmd::kThreads - 1) / rmd::kThreads, d->batch, d->levels);
+    hipStream_t st = rmd::as_stream(stream);
+    switch (radius) {
+#define RMD_CASE(RR) \
+    case RR: rmd::corr_lookup_backward_kernel<RR><<<grid, rmd::kThreads, 0, st>>>(grad_out, g, coords, zero_level_mask, grad_levels); break;
+        RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
+#undef RMD_CASE
+        default:
+            rmd::set_error("rmd_corr_lookup_backward: radius %d not in 1..8", radius);
+            return RMD_ERR_SHAPE;
+    }
+    return rmd::check_launch("rmd_corr_lookup_backward");
+}
+
+extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,
+                                     float scale, float* pooled, void* stream) {
+    RMD_REQUIRE(fmap2 && pooled, RMD_ERR_ARG, "rmd_corr_pool_targets: null pointer");
+    int rc = rmd::check_grad_args(batch, channels, height, width, levels);
+    if (rc) return rc;
+    const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
+    const long long total = (long long)batch * g.T * channels;
+    rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
+                               rmd::as_stream(stream)>>>(fmap2, g, channels, scale, pooled);
+    return rmd::check_launch("rmd_corr_pool_targets");
+}
+
+extern "C" int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width,
+                                       int levels, float scale, float* grad_fmap2, void* stream) {
+    RMD_REQUIRE(grad_pooled && grad_fmap2, RMD_ERR_ARG, "rmd_corr_unpool_targets: null pointer");
+    int rc = rmd::check_grad_args(batch, channels, height, width, levels);
+    if (rc) return rc;
+    const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
+    const long long total = (long long)batch * channels * height * width;
+    rmd::unpool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
+                                 rmd::as_stream(stream)>>>(grad_pooled, g, channels, scale, grad_fmap2);
+    return rmd::check_launch("rmd_corr_unpool_targets");
+}

@@ -23,6 +23,7 @@
 #include "rmd_common.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace rmd {
 namespace {
@@ -71,6 +72,26 @@ prep_operand(const float* __restrict__ f, T* __restrict__ o, int C, int N, int C
     const uint4* src = reinterpret_cast<const uint4*>(vals);
 #pragma unroll
     for (int j = 0; j < (int)(16 * sizeof(T) / 16); ++j) dst[j] = src[j];
+}
+
+// prep (w8 GEMM path): fmap1 (B, C, N) f32 -> bf16 in MFMA B-fragment order,
+//   o[b][qt][s][lane][8]  (lane = j + 32h: channels 16s + 8h .. +7 of query min(32 qt + j, N - 1)),
+// so each of a wave's 16 B-fragment loads per 32-query tile is one contiguous 1 KiB read.  Padded
+// queries of the last tile copy query N-1 (their results are stored to N-1: identical bytes).
+__global__ void __launch_bounds__(kThreads)
+prep_bfrag(const float* __restrict__ f, __bf16* __restrict__ o, int C, int N, int nqt) {
+    const int b = blockIdx.y;
+    const int t = blockIdx.x * kThreads + threadIdx.x;
+    const int L = t & 63, s = (t >> 6) & 15, qt = t >> 10;
+    if (qt >= nqt) return;
+    const int j = L & 31, h = L >> 5;
+    const int q = min(qt * 32 + j, N - 1);
+    const int c0 = 16 * s + 8 * h;
+    const float* src = f + ((size_t)b * C + c0) * N + q;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)(c0 + e < C ? src[(size_t)e * N] : 0.f);
+    *reinterpret_cast<bf16x8*>(o + (((size_t)b * nqt + qt) * 1024 + s * 64 + L) * 8) = v;
 }
 
 template <typename TOut> __device__ __forceinline__ TOut cvt_out(float v);
@@ -246,6 +267,14 @@ corr_pyramid_tiled(const typename Operand<F32>::T* __restrict__ opA,   // fmap2 
     }
 }
 
+// LDS swizzle of the A block (256 target rows x 32 16-B chunks): chunk' = chunk ^ swz(row).
+// A ds_read_b128 fragment read serves the lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (and
+// +32) in one LDS cycle each iff their 16 addresses fall in distinct 16-B bank slots.  The lanes
+// of a fragment read rows base + 16*(j>>3) + (j&7) (j = lane & 31) at one chunk, so the slot must
+// separate j&7 AND the parity of j>>3: swz = (row & 7) | ((row >> 4) & 1) << 3.  (row & 15 alone
+// maps j and j+8 to one slot: a 2-way conflict on every fragment read.)
+__device__ __forceinline__ int a_swz(int row) { return (row & 7) | ((row >> 1) & 8); }
+
 // ---------------------------------------------------------------------------------------------
 // Target-stationary kernel (bf16 operands, fp16 pyramid, C = 256): the performance path.
 //
@@ -312,11 +341,11 @@ __device__ __forceinline__ void s_wait_b(bf16x8 (&bq)[16]) {
 
 template <int NT>
 __device__ __forceinline__ void s_lda(bf16x8 (&a)[NT], const unsigned char* smem, const int (&arow)[NT], int s, int h) {
-    constexpr int Cp = 256, SWZ = 15;
+    constexpr int Cp = 256;
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
         const int row = arow[ti];
-        a[ti] = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * Cp * 2 + (((2 * s + h) ^ (row & SWZ)) << 4));
+        a[ti] = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * Cp * 2 + (((2 * s + h) ^ a_swz(row)) << 4));
     }
 }
 
@@ -458,7 +487,7 @@ __global__ void __launch_bounds__(STraits<TH>::kThreads, 1)
 corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
                         __half* __restrict__ pyr, __half* __restrict__ trash_base) {
     using Tr = STraits<TH>;
-    constexpr int Cp = 256, CPR = Cp / 8, SWZ = 15, NT = Tr::kTiles;
+    constexpr int Cp = 256, CPR = Cp / 8, NT = Tr::kTiles;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int H = g.height, W = g.width, N = H * W;
@@ -490,7 +519,7 @@ corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict
         const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
-        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ (row & SWZ)) << 4)) = v;
+        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
     }
     __syncthreads();
 
@@ -539,6 +568,477 @@ corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pipelined target-stationary kernel (bf16 operands, fp16 pyramid, C = 256): the performance path.
+//
+// Same block geometry as corr_pyramid_stationary<2> (4 waves, one per SIMD; a 16x16 target block's
+// A operand in LDS; each wave sweeps its own 32-query tiles against all 256 targets), but the
+// epilogue of tile t is interleaved k-step by k-step with the MFMAs of tile t+1:
+//  * two accumulator sets (2 x 128 AGPRs) ping-pong between "being accumulated" and "being stored";
+//  * k-step s of tile t+1 carries the epilogue piece s of tile t: level-0 row pair s/2, chunk s%2
+//    (one 1 KiB store), the level-1 partial sums of that pair, and every 4th / 8th k-step the
+//    level-1 / level-2 / level-3 stores, so ~27 VALU + 1-2 stores ride along each 8 MFMAs;
+//  * the B fragment of k-step s for tile t+2 is re-loaded into bq[s] right after k-step s's MFMAs
+//    (rolling refill), so each load has a whole tile-phase to land; the waits are hipcc's own;
+//  * stores are raw buffer stores through one descriptor per level covering the wave's valid rows:
+//    the per-lane 32-bit offset = query*chunk bytes + row*row stride, rows past the level and
+//    chunks past the row fall outside num_records / get a 1 GiB bias and are dropped by the
+//    hardware range check — no predication, no redirect;
+//  * lanes of a partial last query tile load (and so compute) query N-1's row and store to it:
+//    identical bytes to the same address, benign.
+namespace pipe {
+
+constexpr unsigned kBig = 0x40000000u;    // offset bias that lands beyond every level's range
+
+struct Lvl {
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned rs;      // row stride (bytes)
+    unsigned cs;      // chunk stride (bytes)
+    unsigned cw2;     // chunk bytes (per query)
+    int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
+};
+
+struct Ctx {
+    Lvl l[4];
+};
+
+__device__ __forceinline__ unsigned pk(float a, float b) {
+    const __half2 v = __floats2half2_rn(a, b);
+    return *reinterpret_cast<const unsigned*>(&v);
+}
+
+__device__ __forceinline__ void swp(unsigned& x, unsigned& y) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+
+// lane-dependent parts of the store offsets for query q (bytes): q * chunk bytes + h * row stride
+struct LaneOff {
+    unsigned o[4];
+};
+
+__device__ __forceinline__ LaneOff lane_offsets(const Ctx& c, int q, int h, bool live) {
+    LaneOff r;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) r.o[l] = live ? (unsigned)q * c.l[l].cw2 + (unsigned)h * c.l[l].rs : kBig;
+    return r;
+}
+
+// uniform part of a store at (row pair base row r0, chunk tc) of level l
+__device__ __forceinline__ unsigned soff(const Lvl& L, int r0, int tc) {
+    return tc < L.chunks ? (unsigned)r0 * L.rs + (unsigned)tc * L.cs : kBig;
+}
+
+// per-tile running sums of the epilogue (unscaled: level-l sums are 4^l x the average)
+struct EpiState {
+    float s1[8][2][2];    // level-1 row yy (0..7), col group cg, pair u
+    float s2[4][2];       // level-2 row, col group
+};
+
+#define V(acc, row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)])
+
+// Epilogue piece s (0..15) of one tile, from accumulator set `acc` (see the block comment).
+template <int S, int AUX = 0>
+__device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, const LaneOff& lo, EpiState& st) {
+    constexpr int m = S >> 1, tc = S & 1;
+    // level 0: rows 2m (lanes h=0) / 2m+1 (lanes h=1) of chunk tc after the half-wave swap
+    {
+        unsigned x0 = pk(V(acc, 2 * m, tc, 0), V(acc, 2 * m, tc, 1));
+        unsigned x1 = pk(V(acc, 2 * m, tc, 2), V(acc, 2 * m, tc, 3));
+        unsigned y0 = pk(V(acc, 2 * m + 1, tc, 0), V(acc, 2 * m + 1, tc, 1));
+        unsigned y1 = pk(V(acc, 2 * m + 1, tc, 2), V(acc, 2 * m + 1, tc, 3));
+        swp(x0, y0);
+        swp(x1, y1);
+        const i32x4 d = {(int)x0, (int)x1, (int)y0, (int)y1};
+        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[0].rsrc, (int)(lo.o[0] + soff(c.l[0], 2 * m, tc)), 0, AUX);
+    }
+    // level-1 sums of level-1 row m, col group tc: cols {2h, 2h+1} (tc 0) / {4+2h, 5+2h} (tc 1)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+        st.s1[m][tc][u] = (V(acc, 2 * m, tc, 2 * u) + V(acc, 2 * m, tc, 2 * u + 1)) +
+                          (V(acc, 2 * m + 1, tc, 2 * u) + V(acc, 2 * m + 1, tc, 2 * u + 1));
+    if constexpr ((S & 3) == 3) {
+        // level-1 rows 2p, 2p+1 complete (p = S >> 2): one store of both rows, lanes h -> row 2p+h
+        constexpr int p = S >> 2;
+        unsigned x0 = pk(0.25f * st.s1[2 * p][0][0], 0.25f * st.s1[2 * p][0][1]);
+        unsigned x1 = pk(0.25f * st.s1[2 * p][1][0], 0.25f * st.s1[2 * p][1][1]);
+        unsigned y0 = pk(0.25f * st.s1[2 * p + 1][0][0], 0.25f * st.s1[2 * p + 1][0][1]);
+        unsigned y1 = pk(0.25f * st.s1[2 * p + 1][1][0], 0.25f * st.s1[2 * p + 1][1][1]);
+        swp(x0, y0);
+        swp(x1, y1);
+        const i32x4 d = {(int)x0, (int)y0, (int)x1, (int)y1};
+        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[1].rsrc, (int)(lo.o[1] + soff(c.l[1], 2 * p, 0)), 0, AUX);
+        // level-2 sums of level-2 row p: lane h holds cols {h, 2+h}
+#pragma unroll
+        for (int cg = 0; cg < 2; ++cg)
+            st.s2[p][cg] = (st.s1[2 * p][cg][0] + st.s1[2 * p][cg][1]) + (st.s1[2 * p + 1][cg][0] + st.s1[2 * p + 1][cg][1]);
+    }
+    if constexpr ((S & 7) == 7) {
+        // level-2 rows 2k, 2k+1 complete (k = S >> 3): lanes h -> row 2k+h, 4 cols (8 B)
+        constexpr int k = S >> 3;
+        unsigned x = pk(0.0625f * st.s2[2 * k][0], 0.0625f * st.s2[2 * k][1]);          // row 2k:   cols h, 2+h
+        unsigned y = pk(0.0625f * st.s2[2 * k + 1][0], 0.0625f * st.s2[2 * k + 1][1]);  // row 2k+1: cols h, 2+h
+        swp(x, y);          // lane h now holds row 2k+h: x = cols {0,2}, y = cols {1,3}
+        const i32x2 d = {(int)__builtin_amdgcn_perm(y, x, 0x05040100u), (int)__builtin_amdgcn_perm(y, x, 0x07060302u)};
+        __builtin_amdgcn_raw_buffer_store_b64(d, c.l[2].rsrc, (int)(lo.o[2] + soff(c.l[2], 2 * k, 0)), 0, AUX);
+    }
+    if constexpr (S == 15) {
+        // level 3: rows 0, 1 (level-2 rows 0-1 / 2-3), cols 0, 1 (level-2 cols {0,1} / {2,3});
+        // own partial of col cg is level-2 col 2cg+h; the swap adds the other half's
+        float a0[2], a1[2];
+#pragma unroll
+        for (int cg = 0; cg < 2; ++cg) {
+            a0[cg] = st.s2[0][cg] + st.s2[1][cg];
+            a1[cg] = st.s2[2][cg] + st.s2[3][cg];
+        }
+        unsigned x0 = __float_as_uint(a0[0]), y0 = __float_as_uint(a1[0]);
+        unsigned x1 = __float_as_uint(a0[1]), y1 = __float_as_uint(a1[1]);
+        swp(x0, y0);        // lane h: x0 + y0 = full row-h sum of col 0
+        swp(x1, y1);
+        const float inv = 1.0f / 64.0f;
+        const unsigned v = pk(inv * (__uint_as_float(x0) + __uint_as_float(y0)),
+                              inv * (__uint_as_float(x1) + __uint_as_float(y1)));
+        __builtin_amdgcn_raw_buffer_store_b32((int)v, c.l[3].rsrc, (int)(lo.o[3] + soff(c.l[3], 0, 0)), 0, AUX);
+    }
+}
+#undef V
+
+// A fragments of k-step s for the 8 target tiles (XOR-swizzled LDS rows, see the stationary kernel)
+__device__ __forceinline__ void lda(bf16x8 (&a)[8], const unsigned char* smem, const int (&arow)[8], int s, int h) {
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti) {
+        const int row = arow[ti];
+        a[ti] = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * 512 + (((2 * s + h) ^ a_swz(row)) << 4));
+    }
+}
+
+// interleave hint for one k-step: 8 x {1 MFMA, 1 LDS read, 3 VALU}, then the memory ops
+__device__ __forceinline__ void kstep_schedule() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x040, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+}
+
+// One k-step S of a phase: MFMAs into accM (optional), epilogue piece S of accE (optional),
+// then refill bq[S] from bnext (the next tile).
+template <int S, bool MMA, bool EPI>
+__device__ __forceinline__ void kstep(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
+                                      bf16x8 (&acur)[8], bf16x8 (&anext)[8], const unsigned char* smem,
+                                      const int (&arow)[8], int h, const __bf16* bnext, const Ctx& c,
+                                      const LaneOff& lo, EpiState& st) {
+    if constexpr (MMA) {
+        if constexpr (S + 1 < 16) lda(anext, smem, arow, S + 1, h);
+        const f32x16 zero = {};
+#pragma unroll
+        for (int ti = 0; ti < 8; ++ti)
+            accM[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[ti], bq[S], S == 0 ? zero : accM[ti], 0, 0, 0);
+        bq[S] = *reinterpret_cast<const bf16x8*>(bnext + 16 * S);
+    }
+    if constexpr (EPI) epi_piece<S>(accE, c, lo, st);
+    if constexpr (MMA && EPI) kstep_schedule();
+    __builtin_amdgcn_sched_barrier(0);      // one scheduling region per k-step (bounded live ranges)
+}
+
+template <int S, bool MMA, bool EPI>
+__device__ __forceinline__ void ksteps(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
+                                       bf16x8 (&a0)[8], bf16x8 (&a1)[8], const unsigned char* smem,
+                                       const int (&arow)[8], int h, const __bf16* bnext, const Ctx& c,
+                                       const LaneOff& lo, EpiState& st) {
+    if constexpr (S < 16) {
+        if constexpr (S % 2 == 0) kstep<S, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
+        else kstep<S, MMA, EPI>(accM, accE, bq, a1, a0, smem, arow, h, bnext, c, lo, st);
+        ksteps<S + 1, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
+    }
+}
+
+// one tile-phase: MFMAs of the tile whose B fragments are in bq (if MMA), epilogue of the tile in
+// accE for query qE (if EPI), B fragments of the following tile loaded from bnext
+template <bool MMA, bool EPI>
+__device__ __forceinline__ void phase(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
+                                      const unsigned char* smem, const int (&arow)[8], int h, const __bf16* bnext,
+                                      const Ctx& c, int qE, bool live) {
+    bf16x8 a0[8], a1[8];
+    if constexpr (MMA) lda(a0, smem, arow, 0, h);
+    const LaneOff lo = lane_offsets(c, qE, h, live);
+    EpiState st;
+    ksteps<0, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
+}
+
+}  // namespace pipe
+
+__global__ void __launch_bounds__(256, 1)
+corr_pyramid_pipe(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
+                  __half* __restrict__ pyr, int drop_stores) {
+    constexpr int Cp = 256, CPR = Cp / 8;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int H = g.height, W = g.width, N = H * W;
+    const int ncb = (W + 15) >> 4;
+    const int nblk = ((H + 15) >> 4) * ncb;
+    // XCD-aware bijective remap: consecutive logical blocks (same batch) share an XCD's L2
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tb = lid % nblk;
+    const int rest = lid / nblk;
+    const int split = rest % qsplit;
+    const int b = rest / qsplit;
+    const int rb = tb / ncb, cb = tb - rb * ncb;
+    const int ty0 = rb * 16, tx0 = cb * 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+
+    // ---- A block -> LDS (zero rows for targets outside the image) ------------------------------
+    const __bf16* gA = opA + (size_t)b * N * Cp;
+    for (int id = tid; id < 256 * CPR; id += 256) {
+        const int row = id / CPR, c = id - row * CPR;
+        const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
+        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
+    }
+    __syncthreads();
+
+    int arow[8];
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti) arow[ti] = (4 * (ti >> 1) + (j >> 3)) * 16 + 8 * (ti & 1) + (j & 7);
+
+    // ---- per-level store descriptors of this block (wave-uniform) -------------------------------
+    pipe::Ctx c;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
+        const int y0 = rb * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        const int cw = g.tw[l];
+        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 2u : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
+        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;   // diagnostic: 0 drops every store
+        __half* bp = pyr + base;
+        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+            (int)__builtin_amdgcn_readfirstlane(range), 0x00020000);
+        c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
+        c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
+        c.l[l].cw2 = (unsigned)cw * 2u;
+        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+    }
+
+    // ---- this wave's query tiles: t_k = first + k * stride, k < n -------------------------------
+    const __bf16* gB = opB + (size_t)b * N * Cp + 8 * h;
+    const int nqt = (N + 31) >> 5;
+    const int stride = 4 * qsplit;
+    const int first = split * 4 + w;
+    if (first >= nqt) return;
+    const int n = (nqt - first + stride - 1) / stride;
+    auto qrow = [&](int k) {        // B row of this lane for tile k (clamped: tile and query)
+        const int kk = min(k, n - 1);
+        return gB + (size_t)min((first + kk * stride) * 32 + j, N - 1) * Cp;
+    };
+    auto qidx = [&](int k) { return min((first + k * stride) * 32 + j, N - 1); };
+
+    bf16x8 bq[16];
+    {
+        const __bf16* p0 = qrow(0);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 16 * s);
+    }
+    f32x16 accA[8], accB[8];
+    // phases: MFMA of tile k alongside the epilogue of tile k-1.  Uniform two-phase loop body (the
+    // accumulator sets never move); a trailing tile index >= n computes on clamped rows and its
+    // epilogue stores are dropped (live = false -> offsets beyond every range).
+    pipe::phase<true, false>(accA, accB, bq, smem, arow, h, qrow(1), c, 0, false);      // MFMA tile 0
+    for (int k = 1; k <= n; k += 2) {
+        pipe::phase<true, true>(accB, accA, bq, smem, arow, h, qrow(k + 1), c, qidx(k - 1), true);
+        pipe::phase<true, true>(accA, accB, bq, smem, arow, h, qrow(k + 2), c, qidx(min(k, n - 1)), k < n);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 8-wave target-stationary kernel (bf16 operands, fp16 pyramid, C = 256).
+//
+// Same block geometry and epilogue as corr_pyramid_pipe, but two waves per SIMD instead of one
+// software-pipelined wave: each of the 8 waves owns whole 256-target x 32-query tiles (its own
+// query tiles, no duplicated B loads) and runs MFMAs then the epilogue serially; the SIMD's other
+// wave fills the matrix pipe while one stores.  Register budget 256 per wave: one accumulator set
+// (128), B fragments (64), A fragments single-buffered (32: the k-step s+1 fragment of tile ti is
+// read right after tile ti's k-step-s MFMA has consumed the register).
+namespace w8 {
+
+// A fragment of target tile ti at k-step s lives at LDS byte
+//   lane_base + ((2s ^ c) << 4) + tile_off(ti),   lane_base = (16 (j>>3) + (j&7)) * 512,
+// c = h ^ a_swz(row) (the swizzle of a fragment row does not depend on ti), tile_off(ti) =
+// (64 (ti>>1) + 8 (ti&1)) * 512 — so one address VGPR per k-step (two: tile_off of ti >= 4 passes
+// the 16-bit ds offset) and the tile offset in the instruction's immediate.
+template <int S>
+__device__ __forceinline__ unsigned step_addr(unsigned lane_base, unsigned c) {
+    return lane_base + (((unsigned)(2 * S) ^ c) << 4);
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const unsigned char* smem, unsigned v0, int ti) {
+    const unsigned off = (unsigned)(64 * (ti >> 1) + 8 * (ti & 1)) * 512u;
+    return *reinterpret_cast<const bf16x8*>(smem + v0 + off);
+}
+
+template <int S>
+__device__ __forceinline__ void mma_steps(f32x16 (&acc)[8], const bf16x8 (&bq)[16], bf16x8 (&a)[8],
+                                          const unsigned char* smem, unsigned lane_base, unsigned c) {
+    if constexpr (S < 16) {
+        const f32x16 zero = {};
+        const unsigned vn = step_addr<(S + 1) & 15>(lane_base, c);
+#pragma unroll
+        for (int ti = 0; ti < 8; ++ti) {
+            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ti], bq[S], S == 0 ? zero : acc[ti], 0, 0, 0);
+            if constexpr (S + 1 < 16) a[ti] = lds_frag(smem, vn, ti);     // single-buffered: reuse a[ti]
+        }
+        mma_steps<S + 1>(acc, bq, a, smem, lane_base, c);
+    }
+}
+
+__device__ __forceinline__ void mma(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
+                                    unsigned lane_base, unsigned c) {
+    // keep the per-k-step addresses inside the tile loop (hoisted, 16-32 of them would spill)
+    asm volatile("" : "+v"(lane_base), "+v"(c));
+    bf16x8 a[8];
+    const unsigned v0 = step_addr<0>(lane_base, c);
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti) a[ti] = lds_frag(smem, v0, ti);
+    mma_steps<0>(acc, bq, a, smem, lane_base, c);
+}
+
+template <int S, int AUX>
+__device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx& c, const pipe::LaneOff& lo,
+                                         pipe::EpiState& st) {
+    if constexpr (S < 16) {
+        pipe::epi_piece<S, AUX>(acc, c, lo, st);
+        epilogue<S + 1, AUX>(acc, c, lo, st);
+    }
+}
+
+}  // namespace w8
+
+template <int AUX>
+__global__ void __launch_bounds__(512, 1)
+corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
+                __half* __restrict__ pyr, int drop_stores) {
+    constexpr int Cp = 256, CPR = Cp / 8, WAVES = 8;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int H = g.height, W = g.width, N = H * W;
+    const int ncb = (W + 15) >> 4;
+    const int nblk = ((H + 15) >> 4) * ncb;
+    const int nwg = gridDim.x;
+    const int orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int tb = lid % nblk;
+    const int rest = lid / nblk;
+    const int split = rest % qsplit;
+    const int b = rest / qsplit;
+    const int rb = tb / ncb, cb = tb - rb * ncb;
+    const int ty0 = rb * 16, tx0 = cb * 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+
+    const __bf16* gA = opA + (size_t)b * N * Cp;
+    for (int id = tid; id < 256 * CPR; id += 64 * WAVES) {
+        const int row = id / CPR, c = id - row * CPR;
+        const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
+        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
+    }
+    __syncthreads();
+
+    const unsigned lane_row = 16u * (j >> 3) + (j & 7);
+    const unsigned lane_base = lane_row * 512u;
+    const unsigned lane_c = (unsigned)(h ^ a_swz((int)lane_row));
+
+    pipe::Ctx c;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
+        const int y0 = rb * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        const int cw = g.tw[l];
+        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 2u : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
+        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;
+        __half* bp = pyr + base;
+        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+            (int)__builtin_amdgcn_readfirstlane(range), 0x00020000);
+        c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
+        c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
+        c.l[l].cw2 = (unsigned)cw * 2u;
+        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+    }
+
+    const int nqt = (N + 31) >> 5;
+    // B operand in fragment order (prep_bfrag): tile qt, k-step s = 1 KiB at ((b nqt + qt) 16 + s) KiB
+    const __bf16* gB = opB + ((size_t)b * nqt * 1024 + lane) * 8;
+    const int stride = WAVES * qsplit;
+    int qt = split * WAVES + w;
+    if (qt >= nqt) return;
+    bf16x8 bq[16];
+    {
+        const __bf16* p0 = gB + (size_t)qt * 8192;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 512 * s);
+    }
+    while (true) {
+        f32x16 acc[8];
+        w8::mma(acc, bq, smem, lane_base, lane_c);
+        const int qn = qt + stride;
+        // next tile's B fragments issue before this tile's stores, so waiting for them never
+        // waits for the stores (vmcnt counts in issue order)
+        const __bf16* pn = gB + (size_t)min(qn, nqt - 1) * 8192;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
+        const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+        pipe::EpiState st;
+        w8::epilogue<0, AUX>(acc, c, lo, st);
+        if (qn >= nqt) break;
+        qt = qn;
+    }
+}
+
+// GEMM path for a call: the w8 kernel (default) needs bf16 operands, an fp16 pyramid, C <= 256 and
+// 32-bit store offsets; RMD_GEMM_KERNEL = pipe | stationary | tiled selects the others (diagnostic).
+enum class Path { W8, PIPE, STATIONARY, TILED };
+
+Path gemm_path(const rmd_pyramid_desc& d, int C, int compute) {
+    const int Cp = (C + kKC - 1) / kKC * kKC;
+    const char* k_env = getenv("RMD_GEMM_KERNEL");
+    if (compute != RMD_BF16 || d.storage != RMD_F16 || Cp != 256 || getenv("RMD_FORCE_TILED_GEMM") ||
+        (k_env && strcmp(k_env, "tiled") == 0))
+        return Path::TILED;
+    const long long N = (long long)d.height * d.width;
+    const double span0 = 16.0 * d.tiles_x[0] * (double)N * 8 * 2;     // one wave's 16 level-0 rows (bytes)
+    if (span0 >= (double)(1u << 30)) return Path::STATIONARY;
+    if (k_env && strcmp(k_env, "stationary") == 0) return Path::STATIONARY;
+    if (k_env && strcmp(k_env, "pipe") == 0) return Path::PIPE;
+    return Path::W8;
+}
+
 template <bool F32>
 int launch_prepare(const float* f1, const float* f2, int C, const rmd_pyramid_desc& d, void* workspace,
                    hipStream_t st) {
@@ -552,6 +1052,13 @@ int launch_prepare(const float* f1, const float* f2, int C, const rmd_pyramid_de
     // e.g. the reference's 256); the f32 parity path scales the f32 accumulators in the epilogue
     const float prescale = F32 ? 1.0f : 1.0f / sqrtf((float)C);
     prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp, prescale);
+    if constexpr (!F32) {
+        if (gemm_path(d, C, RMD_BF16) == Path::W8) {
+            const int nqt = (N + 31) / 32;
+            prep_bfrag<<<dim3((nqt * 1024 + kThreads - 1) / kThreads, d.batch), kThreads, 0, st>>>(f1, opB, C, N, nqt);
+            return check_launch("rmd_corr_prepare");
+        }
+    }
     prep_operand<T><<<pg, kThreads, 0, st>>>(f1, opB, C, N, Cp, 1.0f);
     return check_launch("rmd_corr_prepare");
 }
@@ -566,7 +1073,7 @@ int launch_pyramid(int C, const rmd_pyramid_desc& d, void* pyramid, void* worksp
     const float scale = 1.0f / sqrtf((float)C);
     const PyrGeom geom = make_geom(d);
     if constexpr (!F32 && sizeof(TOut) == 2) {
-        if (Cp == 256 && !getenv("RMD_FORCE_TILED_GEMM")) {
+        if (gemm_path(d, C, RMD_BF16) != Path::TILED) {
             const int nblk = ((d.height + 15) / 16) * ((d.width + 15) / 16);
             const int nqt = (N + 31) / 32;
             int qsplit = 1;
@@ -574,7 +1081,28 @@ int launch_pyramid(int C, const rmd_pyramid_desc& d, void* pyramid, void* worksp
             const int lds = 256 * Cp * 2;
             const int nwg = nblk * d.batch * qsplit;
             __half* out = reinterpret_cast<__half*>(pyramid);
-            __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * N * Cp);
+            __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * nqt * 32 * Cp);
+            const Path path = gemm_path(d, C, RMD_BF16);
+            if (path == Path::W8) {
+                const char* ab = getenv("RMD_ABLATE");
+                // stores are non-temporal (aux bit 1, nt): measured 0.24 vs 0.26 ms plain at cfg2 (the
+                // pyramid is written once and read back a full GEMM later); RMD_STORE_AUX overrides
+                const char* aux_env = getenv("RMD_STORE_AUX");
+                const int aux = aux_env ? atoi(aux_env) : 2;
+                int qs = 1;
+                while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
+                auto kern = aux == 2 ? corr_pyramid_w8<2> : aux == 3 ? corr_pyramid_w8<3> : corr_pyramid_w8<0>;
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, ab && atoi(ab) == 1);
+                return check_launch("rmd_corr_pyramid/gemm-w8");
+            }
+            if (path == Path::PIPE) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_pipe),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                const char* ab = getenv("RMD_ABLATE");
+                corr_pyramid_pipe<<<nwg, 256, lds, st>>>(opA, opB, geom, qsplit, out, ab && atoi(ab) == 1);
+                return check_launch("rmd_corr_pyramid/gemm-pipe");
+            }
             const char* abl_env = getenv("RMD_ABLATE");
             const int abl = abl_env ? atoi(abl_env) : 0;
             const char* w_env = getenv("RMD_GEMM_WAVES");           // 4 (default) or 8
@@ -616,7 +1144,8 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     if (!d || channels <= 0) return 0;
     const size_t Cp = (size_t)(channels + rmd::kKC - 1) / rmd::kKC * rmd::kKC;
     const size_t es = compute == RMD_F32 ? 4 : 2;
-    return 2 * (size_t)d->batch * d->height * d->width * Cp * es + 32 * 1024;   // + trash slots (<= 32 x 1 KiB)
+    const size_t N = (size_t)d->height * d->width, Npad = (N + 31) / 32 * 32;   // B operand padded to 32-query tiles
+    return (size_t)d->batch * (N + Npad) * Cp * es + 32 * 1024;                  // + trash slots (<= 32 x 1 KiB)
 }
 
 extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,

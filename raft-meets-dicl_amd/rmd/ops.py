@@ -125,6 +125,110 @@ def corr_lookup(pyr, coords, radius, mask_costs=()):
     return out
 
 
+# ---- RAFT correlation autograd (training) -------------------------------------------------------
+#
+# The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an
+# input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
+# accumulates into ONE dense fp32 gradient G (B, N, T) shared through _CorrState (include/rmd.h,
+# rmd_corr_lookup_backward); the pyramid backward then turns G into d fmap1 / d fmap2 with two plain
+# library GEMMs (hipBLASLt, strided, no copies) and the native pool / unpool kernels.
+
+class _CorrState:
+    def __init__(self, pyr, f1, f2):
+        self.pyr = pyr
+        self.f1 = f1
+        self.f2 = f2
+        self.grad = None          # dense G, allocated by the first lookup backward
+
+
+def _mask_bits(mask_costs, levels):
+    mask = 0
+    for m in mask_costs:
+        if 0 <= m - 3 < levels:
+            mask |= 1 << (m - 3)
+    return mask
+
+
+class _CorrPyramidFn(torch.autograd.Function):
+    """Autograd node of raft.CorrBlock.__init__ (raft.py:18-47)."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, state):
+        ctx.state = state
+        return fmap1.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _gtoken):
+        st = ctx.state
+        f1, f2 = st.f1, st.f2
+        b, c, h, w = f1.shape
+        n = h * w
+        levels = st.pyr.levels
+        if st.grad is None:
+            return torch.zeros_like(f1), torch.zeros_like(f2), None
+        lib = _lib.lib()
+        t = lib.rmd_corr_grad_targets(h, w, levels)
+        scale = 1.0 / float(c) ** 0.5
+        pooled = torch.empty((b, t, c), dtype=torch.float32, device=f1.device)
+        g2 = torch.empty_like(f2)
+        with torch.cuda.device(f1.device):
+            stream = _stream(f1)
+            _lib.check(lib.rmd_corr_pool_targets(_ptr(f2), b, c, h, w, levels, scale, _ptr(pooled), stream),
+                       "rmd_corr_pool_targets")
+            G = st.grad.view(b, n, t)
+            g1 = torch.bmm(pooled.transpose(1, 2), G.transpose(1, 2))                  # (B, C, N)
+            dpool = torch.bmm(G.transpose(1, 2), f1.view(b, c, n).transpose(1, 2))     # (B, T, C)
+            _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
+                       "rmd_corr_unpool_targets")
+        st.grad = None
+        return g1.view(b, c, h, w), g2, None
+
+
+class _CorrLookupFn(torch.autograd.Function):
+    """Autograd node of raft.CorrBlock.__call__ (raft.py:49-95); coords carry no gradient (raft.py:402)."""
+
+    @staticmethod
+    def forward(ctx, token, coords, state, radius, mask_costs):
+        out = corr_lookup(state.pyr, coords, radius, mask_costs)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.mask = _mask_bits(mask_costs, state.pyr.levels)
+        ctx.save_for_backward(coords.detach().float().contiguous())
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (co,) = ctx.saved_tensors
+        st = ctx.state
+        d = st.pyr.desc
+        lib = _lib.lib()
+        if st.grad is None:
+            t = lib.rmd_corr_grad_targets(d.height, d.width, d.levels)
+            st.grad = torch.zeros(d.batch * d.height * d.width * t, dtype=torch.float32, device=co.device)
+        g = gout.float().contiguous()
+        with torch.cuda.device(co.device):
+            _lib.check(lib.rmd_corr_lookup_backward(_ptr(g), ctx_desc(st), _ptr(co), ctx.radius, ctx.mask,
+                                                    _ptr(st.grad), _stream(co)), "rmd_corr_lookup_backward")
+        return gout.new_zeros(()), None, None, None, None
+
+
+def ctx_desc(st):
+    return ctypes.byref(st.pyr.desc)
+
+
+def corr_block_autograd(fmap1, fmap2, levels, precision):
+    """Pyramid + autograd token for a CorrBlock whose feature maps require gradients."""
+    _require_gpu(fmap1, fmap2)
+    pyr = corr_pyramid(fmap1, fmap2, levels, precision)
+    st = _CorrState(pyr, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous())
+    token = _CorrPyramidFn.apply(fmap1, fmap2, st)
+    return pyr, st, token
+
+
+def corr_lookup_autograd(token, state, coords, radius, mask_costs=()):
+    return _CorrLookupFn.apply(token, coords, state, radius, tuple(mask_costs))
+
+
 # ---- DICL cost volumes and DAP ------------------------------------------------------------------
 
 def _stream(t):

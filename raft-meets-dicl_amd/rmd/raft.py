@@ -3,7 +3,15 @@
 Same constructor and call signature; the all-pairs volume and its pooled pyramid are built by one
 MFMA GEMM launch with a pooling epilogue (rmd_corr_pyramid) and each lookup is one bandwidth-bound
 gather launch (rmd_corr_lookup).  Output: contiguous float32 (B, L*(2r+1)^2, H, W), as raft.py:95.
+
+Training: when the feature maps require gradients (and grad mode is on) the block is an autograd
+node — the lookups' backward passes accumulate one dense pyramid gradient (rmd_corr_lookup_backward)
+and the pyramid's backward turns it into d fmap1 / d fmap2 (ops._CorrPyramidFn), matching the
+reference's autograd through grid_sample / avg_pool2d / matmul.  Coordinates get no gradient
+(the reference detaches them, raft.py:402).
 """
+
+import torch
 
 from . import ops
 
@@ -15,7 +23,12 @@ class CorrBlock:
         self.num_levels = num_levels
         self.radius = radius
         self.precision = precision or ops.get_default_precision()
-        self.pyramid = ops.corr_pyramid(fmap1, fmap2, num_levels, self.precision)
+        self._state = self._token = None
+        if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
+            self.pyramid, self._state, self._token = ops.corr_block_autograd(fmap1, fmap2, num_levels,
+                                                                             self.precision)
+        else:
+            self.pyramid = ops.corr_pyramid(fmap1, fmap2, num_levels, self.precision)
 
     @property
     def corr_pyramid(self):
@@ -23,4 +36,6 @@ class CorrBlock:
         return [self.pyramid.unpack(i) for i in range(self.num_levels)]
 
     def __call__(self, coords, mask_costs=[]):
+        if self._token is not None and torch.is_grad_enabled():
+            return ops.corr_lookup_autograd(self._token, self._state, coords, self.radius, mask_costs)
         return ops.corr_lookup(self.pyramid, coords, self.radius, mask_costs)

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""A/B timing of the cfg2 correlation-GEMM kernels (diagnostic; MI355X only, not product code).
+
+For each kernel named in RMD_GEMM_KERNEL values (pipe = default path, stationary = previous one)
+times rmd_corr_pyramid_prepared alone with HIP events on the launch stream and checks that every
+variant's pyramid is bitwise identical to the first one's (same MFMA and pooling order).
+usage: gemm_ab.py [reps]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from rmd import ops  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    dev = torch.device("cuda", 0)
+    f1, f2, _ = bench.synthetic(8, 256, 55, 128, 1, 1234, dev)
+    res, ref = {}, None
+    for name in os.environ.get("RMD_AB", "pipe,stationary").split(","):
+        kern, _, abl = name.partition(":")          # e.g. "pipe:1" = RMD_ABLATE=1 (stores dropped)
+        kern, _, aux = kern.partition("@")          # e.g. "w8@2" = RMD_STORE_AUX=2
+        os.environ["RMD_GEMM_KERNEL"] = kern
+        os.environ["RMD_ABLATE"] = abl or "0"
+        os.environ["RMD_STORE_AUX"] = aux or "2"
+        ev = []
+        for _ in range(3):
+            pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
+        torch.cuda.synchronize()
+        for _ in range(reps):
+            pyr = ops.corr_pyramid(f1, f2, 4, "bf16", events=ev)
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ev)
+        res[name] = {"median_ms": ms[len(ms) // 2], "min_ms": ms[0],
+                     "write_TBps": pyr.data.numel() * 2 / (ms[len(ms) // 2] * 1e-3) / 1e12}
+        if abl:
+            continue
+        if ref is None:
+            ref = pyr.data.clone()
+        else:
+            diff = (pyr.data.view(torch.int16) != ref.view(torch.int16)).sum().item()
+            res[name]["bitwise_mismatch_vs_first"] = int(diff)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
