@@ -106,6 +106,64 @@ def test_lookup_deterministic_and_pyramid_reusable():
     assert not torch.equal(a, c2)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_corr_block_backward_matches_reference_golden(precision):
+    """a11: d(sum(out * grad_out)) / d(fmap1, fmap2) vs the reference's autograd (golden), radius 4,
+    4 levels.  The gradient does not depend on the stored pyramid values, so both precision modes
+    meet the fp32 gate (1e-4)."""
+    import rmd
+    g = load_golden("corr_b2_c32_24x40")
+    f1 = _t(g["fmap1"]).requires_grad_(True)
+    f2 = _t(g["fmap2"]).requires_grad_(True)
+    cb = rmd.raft.CorrBlock(f1, f2, 4, 4, precision=precision)
+    out = cb(_t(g["coords"]))
+    (out * _t(g["grad_out"])).sum().backward()
+    assert rel_max_err(f1.grad.cpu().numpy(), g["grad_fmap1"]) < 1e-4
+    assert rel_max_err(f2.grad.cpu().numpy(), g["grad_fmap2"]) < 1e-4
+
+
+def test_corr_block_backward_accumulates_over_iterations_and_masks():
+    """Several lookups of one block (the GRU iterations) sum their gradients into one pyramid
+    gradient; masked levels contribute nothing; coords receive none.  Oracle: float64 restatement."""
+    import rmd
+    rng = np.random.default_rng(4)
+    b, c, h, w = 2, 48, 19, 26
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    grid = np.stack([xs, ys])[None].astype(np.float64)
+    t1, t2 = _t(f1).requires_grad_(True), _t(f2).requires_grad_(True)
+    cb = rmd.raft.CorrBlock(t1, t2, 4, 3, precision="fp32")
+    loss = 0.0
+    ref1 = np.zeros((b, c, h, w))
+    ref2 = np.zeros((b, c, h, w))
+    cots = []
+    for mask in ([], [4], [3, 6]):
+        co = (grid + rng.normal(0, 3, (b, 2, h, w))).astype(np.float32)
+        go = rng.standard_normal((b, 4 * 49, h, w)).astype(np.float32)
+        cot = _t(co).requires_grad_(True)
+        cots.append(cot)
+        loss = loss + (cb(cot, mask) * _t(go)).sum()
+        r1, r2 = oracle.corr_lookup_backward(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64),
+                                             4, 3, go.astype(np.float64), mask)
+        ref1 += r1
+        ref2 += r2
+    loss.backward()
+    assert rel_max_err(t1.grad.cpu().numpy(), ref1) < 1e-4
+    assert rel_max_err(t2.grad.cpu().numpy(), ref2) < 1e-4
+    assert all(c.grad is None for c in cots)
+
+
+def test_corr_block_no_grad_builds_no_autograd_state():
+    import rmd
+    f1, f2, co = _cfg2_inputs(seed=1, b=1)
+    t1 = _t(f1).requires_grad_(True)
+    with torch.no_grad():
+        cb = rmd.raft.CorrBlock(t1, _t(f2), 4, 4, precision="bf16")
+        out = cb(_t(co))
+    assert cb._token is None and not out.requires_grad
+
+
 def test_zero_flow_centre_channel_is_self_correlation():
     """Property: at integer coords = grid, level-0 centre tap (a=b=r) is f1_p . f2_p / sqrt(C)."""
     import rmd
