@@ -76,24 +76,26 @@ size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* desc, int channe
 
 /*
  * All-pairs correlation + pooled pyramid.  Replaces raft.CorrBlock.__init__
- * (src/models/impls/raft.py:18-47): corr0 = fmap1^T fmap2 / sqrt(C) over each batch, then
- * levels-1 successive 2x2 average pools over the target dims, floor sizes.
+ * (src/models/impls/raft.py:18-47): corr0 = scale * fmap1^T fmap2 over each batch, then
+ * levels-1 successive 2x2 average pools over the target dims, floor sizes.  scale = 1/sqrt(C) is
+ * raft.CorrBlock (raft.py:33); scale = 1 gives raft_fs.CorrBlock's unnormalised products
+ * (src/models/impls/raft_fs.py:13-87, whose pooled-feature dot equals the pooled volume).
  *   compute = RMD_F32  : exact f32 MFMA (v_mfma_f32_32x32x2_f32), the parity mode
  *   compute = RMD_BF16 : bf16 MFMA operands, f32 accumulation (performance mode)
  * All levels are produced by the GEMM epilogue from the f32 accumulators and stored as
  * desc->storage.
  */
-int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels,
+int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, float scale,
                      const rmd_pyramid_desc* desc, int compute, void* pyramid, void* workspace,
                      void* stream);
 
 /* The two halves of rmd_corr_pyramid, for callers that time or overlap them separately:
  * rmd_corr_prepare transposes/converts both feature maps into the workspace (pixel-major,
  * channel-contiguous operands); rmd_corr_pyramid_prepared runs the GEMM + pyramid epilogue on them. */
-int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* desc,
-                     int compute, void* workspace, void* stream);
-int rmd_corr_pyramid_prepared(int channels, const rmd_pyramid_desc* desc, int compute, void* pyramid,
-                              void* workspace, void* stream);
+int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, float scale,
+                     const rmd_pyramid_desc* desc, int compute, void* workspace, void* stream);
+int rmd_corr_pyramid_prepared(int channels, float scale, const rmd_pyramid_desc* desc, int compute,
+                              void* pyramid, void* workspace, void* stream);
 
 /*
  * Windowed bilinear pyramid lookup.  Replaces raft.CorrBlock.__call__ (raft.py:49-95):

@@ -1040,17 +1040,18 @@ Path gemm_path(const rmd_pyramid_desc& d, int C, int compute) {
 }
 
 template <bool F32>
-int launch_prepare(const float* f1, const float* f2, int C, const rmd_pyramid_desc& d, void* workspace,
-                   hipStream_t st) {
+int launch_prepare(const float* f1, const float* f2, int C, float scale, const rmd_pyramid_desc& d,
+                   void* workspace, hipStream_t st) {
     using T = typename Operand<F32>::T;
     const int N = d.height * d.width;
     const int Cp = (C + kKC - 1) / kKC * kKC;
     T* opA = reinterpret_cast<T*>(workspace);
     T* opB = opA + (size_t)d.batch * N * Cp;
     dim3 pg((N + 63) / 64, Cp / 64, d.batch);
-    // bf16 perf path: the 1/sqrt(C) scale is folded into fmap2 before rounding (exact for C = 4^k,
-    // e.g. the reference's 256); the f32 parity path scales the f32 accumulators in the epilogue
-    const float prescale = F32 ? 1.0f : 1.0f / sqrtf((float)C);
+    // bf16 perf path: the scale (1/sqrt(C) for raft.CorrBlock) is folded into fmap2 before rounding
+    // (exact for a power of two, e.g. C = 256 or raft_fs's 1); the f32 parity path scales the f32
+    // accumulators in the epilogue
+    const float prescale = F32 ? 1.0f : scale;
     prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp, prescale);
     if constexpr (!F32) {
         if (gemm_path(d, C, RMD_BF16) == Path::W8) {
@@ -1064,13 +1065,12 @@ int launch_prepare(const float* f1, const float* f2, int C, const rmd_pyramid_de
 }
 
 template <bool F32, typename TOut>
-int launch_pyramid(int C, const rmd_pyramid_desc& d, void* pyramid, void* workspace, hipStream_t st) {
+int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid, void* workspace, hipStream_t st) {
     using T = typename Operand<F32>::T;
     const int N = d.height * d.width;
     const int Cp = (C + kKC - 1) / kKC * kKC;
     T* opA = reinterpret_cast<T*>(workspace);
     T* opB = opA + (size_t)d.batch * N * Cp;
-    const float scale = 1.0f / sqrtf((float)C);
     const PyrGeom geom = make_geom(d);
     if constexpr (!F32 && sizeof(TOut) == 2) {
         if (gemm_path(d, C, RMD_BF16) != Path::TILED) {
@@ -1148,32 +1148,32 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     return (size_t)d->batch * (N + Npad) * Cp * es + 32 * 1024;                  // + trash slots (<= 32 x 1 KiB)
 }
 
-extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,
-                                int compute, void* workspace, void* stream) {
+extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, float scale,
+                                const rmd_pyramid_desc* d, int compute, void* workspace, void* stream) {
     RMD_REQUIRE(fmap1 && fmap2 && workspace, RMD_ERR_ARG, "rmd_corr_prepare: null pointer");
     int rc = rmd::check_args(d, channels, compute);
     if (rc) return rc;
     hipStream_t st = rmd::as_stream(stream);
-    return compute == RMD_BF16 ? rmd::launch_prepare<false>(fmap1, fmap2, channels, *d, workspace, st)
-                               : rmd::launch_prepare<true>(fmap1, fmap2, channels, *d, workspace, st);
+    return compute == RMD_BF16 ? rmd::launch_prepare<false>(fmap1, fmap2, channels, scale, *d, workspace, st)
+                               : rmd::launch_prepare<true>(fmap1, fmap2, channels, scale, *d, workspace, st);
 }
 
-extern "C" int rmd_corr_pyramid_prepared(int channels, const rmd_pyramid_desc* d, int compute, void* pyramid,
-                                         void* workspace, void* stream) {
+extern "C" int rmd_corr_pyramid_prepared(int channels, float scale, const rmd_pyramid_desc* d, int compute,
+                                         void* pyramid, void* workspace, void* stream) {
     RMD_REQUIRE(pyramid && workspace, RMD_ERR_ARG, "rmd_corr_pyramid_prepared: null pointer");
     int rc = rmd::check_args(d, channels, compute);
     if (rc) return rc;
     hipStream_t st = rmd::as_stream(stream);
     if (compute == RMD_BF16)
-        return d->storage == RMD_F16 ? rmd::launch_pyramid<false, __half>(channels, *d, pyramid, workspace, st)
-                                     : rmd::launch_pyramid<false, float>(channels, *d, pyramid, workspace, st);
-    return d->storage == RMD_F16 ? rmd::launch_pyramid<true, __half>(channels, *d, pyramid, workspace, st)
-                                 : rmd::launch_pyramid<true, float>(channels, *d, pyramid, workspace, st);
+        return d->storage == RMD_F16 ? rmd::launch_pyramid<false, __half>(channels, scale, *d, pyramid, workspace, st)
+                                     : rmd::launch_pyramid<false, float>(channels, scale, *d, pyramid, workspace, st);
+    return d->storage == RMD_F16 ? rmd::launch_pyramid<true, __half>(channels, scale, *d, pyramid, workspace, st)
+                                 : rmd::launch_pyramid<true, float>(channels, scale, *d, pyramid, workspace, st);
 }
 
-extern "C" int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, const rmd_pyramid_desc* d,
-                                int compute, void* pyramid, void* workspace, void* stream) {
-    int rc = rmd_corr_prepare(fmap1, fmap2, channels, d, compute, workspace, stream);
+extern "C" int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, float scale,
+                                const rmd_pyramid_desc* d, int compute, void* pyramid, void* workspace, void* stream) {
+    int rc = rmd_corr_prepare(fmap1, fmap2, channels, scale, d, compute, workspace, stream);
     if (rc) return rc;
-    return rmd_corr_pyramid_prepared(channels, d, compute, pyramid, workspace, stream);
+    return rmd_corr_pyramid_prepared(channels, scale, d, compute, pyramid, workspace, stream);
 }

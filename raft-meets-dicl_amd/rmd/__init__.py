@@ -3,10 +3,15 @@
 Drop-in host mirror of the reference's hot-path modules; every compute call goes through the C ABI
 of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
 
-  rmd.raft.CorrBlock      <- src/models/impls/raft.py:15-95
+  rmd.raft.CorrBlock                    <- src/models/impls/raft.py:15-95
+  rmd.raft_fs.CorrBlock                 <- src/models/impls/raft_fs.py:13-87
+  rmd.corr.make_cmod / CorrelationModule <- src/models/common/corr/{dicl,dicl_1x1,dicl_emb,dot}.py
+  rmd.raft_dicl_ml.CorrelationModule    <- src/models/impls/raft_dicl_ml.py:235-343
+  rmd.blocks.dicl                       <- src/models/common/blocks/dicl.py:93-150
+  rmd.dicl.compute_cost                 <- src/models/impls/dicl.py:212-241
 """
 
-from . import blocks, corr, dicl, ops, raft  # noqa: F401
+from . import blocks, corr, dicl, ops, raft, raft_dicl_ml, raft_fs  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

@@ -44,10 +44,10 @@ _U = ctypes.c_uint
 _SIGS = {
     "rmd_pyramid_describe": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(PyramidDesc)]),
     "rmd_corr_pyramid_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PyramidDesc), _I, _I]),
-    "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
+    "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_lookup": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
-    "rmd_corr_prepare": (_I, [_P, _P, _I, ctypes.POINTER(PyramidDesc), _I, _P, _P]),
-    "rmd_corr_pyramid_prepared": (_I, [_I, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
+    "rmd_corr_prepare": (_I, [_P, _P, _I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P]),
+    "rmd_corr_pyramid_prepared": (_I, [_I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_grad_targets": (ctypes.c_longlong, [_I, _I, _I]),
     "rmd_corr_lookup_backward": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
     "rmd_corr_pool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),

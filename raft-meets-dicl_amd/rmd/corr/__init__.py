@@ -1,6 +1,6 @@
 """Correlation modules — drop-in for src/models/common/corr/__init__.py:7-20 (make_cmod)."""
 
-from . import dicl, dicl_1x1, dicl_emb  # noqa: F401
+from . import dicl, dicl_1x1, dicl_emb, dot  # noqa: F401
 
 
 def make_cmod(type, feature_dim, radius, dap_init="identity", norm_type="batch", relu_inplace=True, **kwargs):
@@ -13,4 +13,6 @@ def make_cmod(type, feature_dim, radius, dap_init="identity", norm_type="batch",
     if type == "dicl-emb":
         return dicl_emb.CorrelationModule(feature_dim=feature_dim, radius=radius, dap_init=dap_init,
                                           norm_type=norm_type, relu_inplace=relu_inplace, **kwargs)
+    if type == "dot":
+        return dot.CorrelationModule(radius=radius, dap_init=dap_init, **kwargs)
     raise ValueError(f"unknown correlation module type '{type}'")

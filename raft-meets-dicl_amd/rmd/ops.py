@@ -48,10 +48,11 @@ _STORAGE_DTYPE = {RMD_F32: torch.float32, RMD_F16: torch.float16}
 class Pyramid:
     """Correlation pyramid in the tiled, query-minor HBM layout of include/rmd.h."""
 
-    def __init__(self, data, desc, channels):
+    def __init__(self, data, desc, channels, scale):
         self.data = data
         self.desc = desc
         self.channels = channels
+        self.scale = scale
 
     @property
     def levels(self):
@@ -73,8 +74,10 @@ class Pyramid:
         return x.float().reshape(b, h, w, 1, hl, wl)
 
 
-def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None):
+def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None):
     """raft.CorrBlock.__init__ (raft.py:18-47) on the GPU -> Pyramid.
+
+    ``scale`` multiplies the products: None = 1/sqrt(C) (raft.py:33), 1.0 = raft_fs.CorrBlock.
 
     ``events`` (optional list) receives (start, end) HIP events bracketing the GEMM launch alone
     (the operand prep runs before the start event) — bench.py's roofline timing.
@@ -86,6 +89,7 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None):
     f1 = fmap1.detach().float().contiguous()
     f2 = fmap2.detach().float().contiguous()
     b, c, h, w = f1.shape
+    scale = 1.0 / float(c) ** 0.5 if scale is None else float(scale)
     d = _lib.describe(b, h, w, levels, storage)
     lib = _lib.lib()
     ws_bytes = lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), c, compute)
@@ -93,17 +97,17 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None):
     data = torch.empty(d.total_elements, dtype=_STORAGE_DTYPE[storage], device=f1.device)
     with torch.cuda.device(f1.device):
         stream = _lib.stream_ptr(f1.device)
-        _lib.check(lib.rmd_corr_prepare(_ptr(f1), _ptr(f2), c, ctypes.byref(d), compute, _ptr(ws), stream),
+        _lib.check(lib.rmd_corr_prepare(_ptr(f1), _ptr(f2), c, scale, ctypes.byref(d), compute, _ptr(ws), stream),
                    "rmd_corr_prepare")
         if events is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        _lib.check(lib.rmd_corr_pyramid_prepared(c, ctypes.byref(d), compute, _ptr(data), _ptr(ws), stream),
+        _lib.check(lib.rmd_corr_pyramid_prepared(c, scale, ctypes.byref(d), compute, _ptr(data), _ptr(ws), stream),
                    "rmd_corr_pyramid_prepared")
         if events is not None:
             e1.record()
             events.append((e0, e1))
-    return Pyramid(data, d, c)
+    return Pyramid(data, d, c, scale)
 
 
 def corr_lookup(pyr, coords, radius, mask_costs=()):
@@ -168,7 +172,7 @@ class _CorrPyramidFn(torch.autograd.Function):
             return torch.zeros_like(f1), torch.zeros_like(f2), None
         lib = _lib.lib()
         t = lib.rmd_corr_grad_targets(h, w, levels)
-        scale = 1.0 / float(c) ** 0.5
+        scale = st.pyr.scale
         pooled = torch.empty((b, t, c), dtype=torch.float32, device=f1.device)
         g2 = torch.empty_like(f2)
         with torch.cuda.device(f1.device):
@@ -216,10 +220,10 @@ def ctx_desc(st):
     return ctypes.byref(st.pyr.desc)
 
 
-def corr_block_autograd(fmap1, fmap2, levels, precision):
+def corr_block_autograd(fmap1, fmap2, levels, precision, scale=None):
     """Pyramid + autograd token for a CorrBlock whose feature maps require gradients."""
     _require_gpu(fmap1, fmap2)
-    pyr = corr_pyramid(fmap1, fmap2, levels, precision)
+    pyr = corr_pyramid(fmap1, fmap2, levels, precision, scale=scale)
     st = _CorrState(pyr, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous())
     token = _CorrPyramidFn.apply(fmap1, fmap2, st)
     return pyr, st, token

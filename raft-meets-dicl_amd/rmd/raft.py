@@ -19,6 +19,8 @@ from . import ops
 class CorrBlock:
     """Correlation volume for matching costs (drop-in for raft.CorrBlock)."""
 
+    scale = None            # 1/sqrt(C) (raft.py:33); raft_fs.CorrBlock overrides with 1.0
+
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, precision=None):
         self.num_levels = num_levels
         self.radius = radius
@@ -26,9 +28,9 @@ class CorrBlock:
         self._state = self._token = None
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
             self.pyramid, self._state, self._token = ops.corr_block_autograd(fmap1, fmap2, num_levels,
-                                                                             self.precision)
+                                                                             self.precision, self.scale)
         else:
-            self.pyramid = ops.corr_pyramid(fmap1, fmap2, num_levels, self.precision)
+            self.pyramid = ops.corr_pyramid(fmap1, fmap2, num_levels, self.precision, scale=self.scale)
 
     @property
     def corr_pyramid(self):

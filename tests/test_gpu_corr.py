@@ -176,3 +176,37 @@ def test_zero_flow_centre_channel_is_self_correlation():
     centre = out[:, 3 * 7 + 3]
     ref = (f1.astype(np.float64) * f2).sum(1) / 8.0
     assert rel_max_err(centre, ref) < 1e-5
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_raft_fs_corr_block_matches_reference_golden(precision):
+    """a4: raft_fs.CorrBlock (pooled-feature window dot, no 1/sqrt(C)) vs the reference's output."""
+    import rmd
+    g = load_golden("corr_fs_b2_c32_24x40")
+    cb = rmd.raft_fs.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), int(g["levels"]), int(g["radius"]),
+                               precision=precision)
+    out = cb(_t(g["coords"]))
+    assert out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == g["out"].shape
+    assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
+
+
+def test_dot_correlation_module_matches_reference_golden():
+    """a5: corr.dot.CorrelationModule forward (with and without DAP) and gradients vs the reference."""
+    import rmd
+    from detinit import det_init
+    g = load_golden("dot_b2_c32_12x16")
+    mod = rmd.corr.make_cmod("dot", 32, int(g["radius"]), dap_init="standard")
+    assert sorted(mod.state_dict().keys()) == sorted(g["sd.keys"].tolist())
+    det_init(mod)
+    mod = mod.to(DEV)
+    f1 = _t(g["fmap1"]).requires_grad_(True)
+    f2 = _t(g["fmap2"]).requires_grad_(True)
+    out = mod(f1, f2, _t(g["coords"]), dap=True)
+    assert rel_max_err(out.detach().cpu().numpy(), g["out"]) < 1e-4
+    d1, d2, dw = torch.autograd.grad(out, (f1, f2, mod.dap.conv1.weight), _t(g["grad_out"]))
+    assert rel_max_err(d1.cpu().numpy(), g["grad_fmap1"]) < 1e-4
+    assert rel_max_err(d2.cpu().numpy(), g["grad_fmap2"]) < 1e-4
+    assert rel_max_err(dw.cpu().numpy(), g["grad_dap"]) < 1e-4
+    with torch.no_grad():
+        nodap = mod(_t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"]), dap=False)
+    assert rel_max_err(nodap.cpu().numpy(), g["out_nodap"]) < 1e-4

@@ -145,3 +145,22 @@ def test_dap_full_324_vs_oracle():
     wt = (rng.standard_normal((324, 324, 1, 1)) * 0.05).astype(np.float32)
     y = rmd.ops.dap(_t(x), _t(wt)).cpu().numpy()
     assert rel_max_err(y, oracle.dap(x.astype(np.float64), wt.astype(np.float64))) < 1e-5
+
+
+@pytest.mark.parametrize("dap_type", ["separate", "full"])
+def test_dicl_ml_correlation_module_golden(dap_type):
+    """a7: raft_dicl_ml.CorrelationModule end to end (gather -> MatchingNet -> mask -> DAP) vs the
+    reference module's output with the same name-keyed weights."""
+    import rmd
+    g = load_golden(f"ml_{dap_type}_b1_c8_8x12")
+    L, r = int(g["levels"]), int(g["radius"])
+    mod = rmd.raft_dicl_ml.CorrelationModule(feature_dim=8, levels=L, radius=r, dap_init="standard",
+                                             dap_type=dap_type)
+    assert sorted(mod.state_dict().keys()) == sorted(g["sd.keys"].tolist())
+    det_init(mod)
+    mod = mod.to(DEV).eval()
+    with torch.no_grad():
+        out = mod([_t(g[f"fmap1_{i}"]) for i in range(L)], [_t(g[f"fmap2_{i}"]) for i in range(L)],
+                  _t(g["coords"]), dap=True, mask_costs=g["mask_costs"].tolist())
+    assert tuple(out.shape) == g["out"].shape
+    assert rel_max_err(out.cpu().numpy(), g["out"]) < 1e-4
