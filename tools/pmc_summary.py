@@ -20,8 +20,8 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        key = "gemm" if "corr_pyramid_stationary" in name or "corr_pyramid_tiled" in name else \
-              "lookup" if "corr_lookup_kernel" in name else "prep" if "prep_operand" in name else None
+        key = "gemm" if "corr_pyramid_" in name else \
+              "lookup" if "corr_lookup_kernel" in name else "prep" if "prep_" in name else None
         if key:
             vals.setdefault(key, []).append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in vals.items()}
