@@ -94,6 +94,81 @@ prep_bfrag(const float* __restrict__ f, __bf16* __restrict__ o, int C, int N, in
     *reinterpret_cast<bf16x8*>(o + (((size_t)b * nqt + qt) * 1024 + s * 64 + L) * 8) = v;
 }
 
+// prep (w8 GEMM path, both operands in one launch): grid (128-pixel tiles, B, 2).  z = 0: fmap2 ->
+// A operand (B, N, 256) bf16 * scale; z = 1: fmap1 -> B operand in fragment order (prep_bfrag's
+// layout).  Read phase: a thread loads 8 channels x 4 pixels (float4 per channel row: a wave reads
+// 2 x 512 B contiguous per instruction), converts, and writes the 4 pixels' 16-B channel octets into
+// a pixel-major bf16 LDS tile.  Write phase: one 16-B fragment per lane-store, the tile's output is
+// one contiguous 64 KiB block for either operand.
+constexpr int kPrepPx = 128, kPrepStride = 256 * 2 + 16;     // LDS row: 256 bf16 + 16 B pad
+
+__global__ void __launch_bounds__(512)
+prep_pair(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* __restrict__ opA,
+          __bf16* __restrict__ opB, int C, int N, int nqt, float scale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int b = blockIdx.y, which = blockIdx.z;
+    const float* f = which ? f1 : f2;
+    const float s = which ? 1.0f : scale;
+    const int t = threadIdx.x;
+    const int p0 = blockIdx.x * kPrepPx;
+    const bool full = p0 + kPrepPx <= N && (N & 3) == 0;
+    const int pl = N - 1 - p0;                       // last valid pixel of the tile (clamp target)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int item = it * 512 + t;               // (channel octet cg, pixel quad q), q fastest
+        const int q = item & 31, cg = item >> 5;
+        float v[8][4];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = cg * 8 + e;
+            const float* src = f + ((size_t)b * C + c) * N + p0 + 4 * q;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c < C) {
+                if (full) {
+                    x = *reinterpret_cast<const float4*>(src);
+                } else {
+                    x.x = src[min(4 * q + 0, pl) - 4 * q];
+                    x.y = src[min(4 * q + 1, pl) - 4 * q];
+                    x.z = src[min(4 * q + 2, pl) - 4 * q];
+                    x.w = src[min(4 * q + 3, pl) - 4 * q];
+                }
+            }
+            v[e][0] = x.x * s;
+            v[e][1] = x.y * s;
+            v[e][2] = x.z * s;
+            v[e][3] = x.w * s;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e][i];
+            *reinterpret_cast<bf16x8*>(lds + (size_t)(4 * q + i) * kPrepStride + cg * 16) = o;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int k = it * 512 + t;                  // 16-B output chunk of the tile's 64 KiB block
+        int px, c0;
+        if (which) {                                 // fragment order per 32-pixel tile: k = (tile, s, lane)
+            const int L = k & 63, st = (k >> 6) & 15;
+            px = (k >> 10) * 32 + (L & 31);
+            c0 = 16 * st + 8 * (L >> 5);
+        } else {                                     // pixel-major: k = px * 32 + octet
+            px = k >> 5;
+            c0 = (k & 31) * 8;
+        }
+        const bf16x8 o = *reinterpret_cast<const bf16x8*>(lds + (size_t)px * kPrepStride + c0 * 2);
+        if (which) {
+            const int qt = blockIdx.x * 4 + (k >> 10);
+            if (qt < nqt) *reinterpret_cast<bf16x8*>(opB + (((size_t)b * nqt + qt) * 1024 + (k & 1023)) * 8) = o;
+        } else if (p0 + px < N) {
+            *reinterpret_cast<bf16x8*>(opA + ((size_t)b * N + p0) * 256 + (size_t)k * 8) = o;
+        }
+    }
+}
+
 template <typename TOut> __device__ __forceinline__ TOut cvt_out(float v);
 template <> __device__ __forceinline__ float cvt_out<float>(float v) { return v; }
 template <> __device__ __forceinline__ __half cvt_out<__half>(float v) { return __float2half_rn(v); }
@@ -1052,14 +1127,16 @@ int launch_prepare(const float* f1, const float* f2, int C, float scale, const r
     // (exact for a power of two, e.g. C = 256 or raft_fs's 1); the f32 parity path scales the f32
     // accumulators in the epilogue
     const float prescale = F32 ? 1.0f : scale;
-    prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp, prescale);
     if constexpr (!F32) {
         if (gemm_path(d, C, RMD_BF16) == Path::W8) {
             const int nqt = (N + 31) / 32;
-            prep_bfrag<<<dim3((nqt * 1024 + kThreads - 1) / kThreads, d.batch), kThreads, 0, st>>>(f1, opB, C, N, nqt);
+            const int lds = kPrepPx * kPrepStride;
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prep_pair), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            prep_pair<<<dim3((N + kPrepPx - 1) / kPrepPx, d.batch, 2), 512, lds, st>>>(f1, f2, opA, opB, C, N, nqt, prescale);
             return check_launch("rmd_corr_prepare");
         }
     }
+    prep_operand<T><<<pg, kThreads, 0, st>>>(f2, opA, C, N, Cp, prescale);
     prep_operand<T><<<pg, kThreads, 0, st>>>(f1, opB, C, N, Cp, 1.0f);
     return check_launch("rmd_corr_prepare");
 }
