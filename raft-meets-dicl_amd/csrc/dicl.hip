@@ -16,6 +16,8 @@
 
 #include "rmd_common.h"
 
+#include <cstdlib>
+
 namespace rmd {
 namespace {
 
@@ -141,6 +143,183 @@ dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (t.wgt[k] != 0.f) atomicAdd(gc + t.idx[k], gv * t.wgt[k]);
+    }
+}
+
+// ---- unit-step fast path ---------------------------------------------------------------------
+// When the sample grid has unit steps (sx = sy = 1: corr/dicl.py and every same-size call), the
+// (2r+1)^2 displacements of pixel p sample (x_p + a - r, y_p + b - r) with ONE fractional weight
+// set, so together they read exactly the (2r+2)^2 integer patch [x0-r, x0+r+1] x [y0-r, y0+r+1]
+// (as the RAFT lookup).  One lane per pixel, all displacements, a loop over channels: per channel
+// the patch is read once (instead of 4 taps x (2r+1)^2 gathers), interpolated separably (x, then y)
+// and the (2r+1)^2 f2 values plus the f1 copies are stored as coalesced 256-B wave rows.
+template <int R>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
+                        StackParams P, float* __restrict__ out) {
+    // 4 consecutive pixels per lane (each with its own patch) so every store is a float4 (1 KiB
+    // per wave-instruction); one channel per thread: grid (pixels/1024, C, B)
+    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * 4;
+    const int c = blockIdx.y, b = blockIdx.z;
+    if (p0 >= n) return;
+    float fx[4], fy[4];
+    int xs[4], ys[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float cx = coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale;
+        float cy = coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale;
+        cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+        cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+        const float fx0 = floorf(cx), fy0 = floorf(cy);
+        fx[k] = cx - fx0;
+        fy[k] = cy - fy0;
+        xs[k] = (int)fx0 - R;
+        ys[k] = (int)fy0 - R;
+    }
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;                       // next displacement plane
+    float* o = out + (size_t)b * D * D * dstride + p0;
+    const float4 v1 = *reinterpret_cast<const float4*>(f1 + ((size_t)b * C + c) * n + p0);
+    const float* f2c = f2 + ((size_t)b * C + c) * nl;
+    float hprev[4][D];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        float hcur[4][D];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int yy = ys[k] + j;
+            const bool rok = yy >= 0 && yy < P.hl;
+            const float* row = f2c + (size_t)min(max(yy, 0), P.hl - 1) * P.wl;
+            float v[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int xx = xs[k] + i;
+                const float e = row[min(max(xx, 0), P.wl - 1)];
+                v[i] = (rok && xx >= 0 && xx < P.wl) ? e : 0.f;
+            }
+#pragma unroll
+            for (int a = 0; a < D; ++a) hcur[k][a] = fmaf(fx[k], v[a + 1] - v[a], v[a]);
+        }
+        if (j > 0) {
+            const int bb = j - 1;
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                float* od = o + (size_t)(a * D + bb) * dstride;
+                *reinterpret_cast<float4*>(od + (size_t)c * n) = v1;
+                float4 r;
+                r.x = fmaf(fy[0], hcur[0][a] - hprev[0][a], hprev[0][a]);
+                r.y = fmaf(fy[1], hcur[1][a] - hprev[1][a], hprev[1][a]);
+                r.z = fmaf(fy[2], hcur[2][a] - hprev[2][a], hprev[2][a]);
+                r.w = fmaf(fy[3], hcur[3][a] - hprev[3][a], hprev[3][a]);
+                *reinterpret_cast<float4*>(od + (size_t)(C + c) * n) = r;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int a = 0; a < D; ++a) hprev[k][a] = hcur[k][a];
+    }
+    if (P.extra && c == 0) {       // dicl_emb.py:81-85: delta (dx = a-r, dy = bb-r) as two constant channels
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+            for (int bb = 0; bb < D; ++bb) {
+                float* od = o + (size_t)(a * D + bb) * dstride;
+                const float dx = (float)(a - R), dy = (float)(bb - R);
+                *reinterpret_cast<float4*>(od + (size_t)(2 * C) * n) = make_float4(dx, dx, dx, dx);
+                *reinterpret_cast<float4*>(od + (size_t)(2 * C + 1) * n) = make_float4(dy, dy, dy, dy);
+            }
+    }
+}
+
+// backward of the unit-step stack: grad_f1[c,p] = sum of the (2r+1)^2 f1-half gradients (plain
+// store); grad_f2 = the f2-half tap gradients spread over p's patch with the forward's separable
+// weights (as rmd_corr_lookup_backward).  The patches of a workgroup's 256 consecutive pixels are
+// summed in LDS (ds_add_f32) over the row window [wy0, wy0 + wrows) starting at the group's lowest
+// patch row; rows past the window go straight to global float atomics; the window is then added
+// to grad_f2 once per element.  grid (pixels/256, C, B).
+constexpr int kWinFloats = 12288;      // 48 KiB LDS window
+
+template <int R>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                                 float* __restrict__ gf1, float* __restrict__ gf2) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    __shared__ float win[kWinFloats];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p < n;
+    float fx = 0.f, fy = 0.f;
+    int xs = 0, ys = 1 << 30;
+    if (pv) {
+        float cx = coords[(size_t)b * 2 * n + p] * P.inv_scale;
+        float cy = coords[(size_t)b * 2 * n + n + p] * P.inv_scale;
+        cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+        cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+        const float fx0 = floorf(cx), fy0 = floorf(cy);
+        fx = cx - fx0;
+        fy = cy - fy0;
+        xs = (int)fx0 - R;
+        ys = (int)fy0 - R;
+    }
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    if (pv) atomicMin(&wmin, max(ys, 0));
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    if (pv) {
+        const float* gp = g + (size_t)b * D * D * dstride + p;
+        float s1 = 0.f;
+        float qprev[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) qprev[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            float qcur[K];
+            if (j < D) {
+                float gr[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const float* gd = gp + (size_t)(a * D + j) * dstride;
+                    s1 += gd[(size_t)c * n];
+                    gr[a] = gd[(size_t)(C + c) * n];
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    qcur[i] = (i < D ? gr[i] * (1.0f - fx) : 0.f) + (i >= 1 ? gr[i - 1] * fx : 0.f);
+            } else {
+#pragma unroll
+                for (int i = 0; i < K; ++i) qcur[i] = 0.f;
+            }
+            const int yy = ys + j;
+            if (yy >= 0 && yy < P.hl) {
+                const bool in_win = yy - wy0 < wrows;
+                float* r = in_win ? win + (size_t)(yy - wy0) * P.wl : g2c + (size_t)yy * P.wl;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const int xx = xs + i;
+                    if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) qprev[i] = qcur[i];
+        }
+        gf1[((size_t)b * C + c) * n + p] = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
     }
 }
 
@@ -276,6 +455,56 @@ dap_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, in
     }
 }
 
+// MFMA form (exact f32: v_mfma_f32_32x32x2_f32 == an fmaf chain): a workgroup owns 32 output
+// displacements x 128 pixels (4 waves x 32 pixels); its 32 rows of W (or of W^T) sit in LDS with an
+// odd row stride, x is read as two 128-B row segments per k-step.  grid (pixels/128, D/32, B).
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__global__ void __launch_bounds__(kThreads)
+dap_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
+                float* __restrict__ out) {
+    extern __shared__ float sw[];                       // 32 rows x (Dk + 1), Dk = D rounded up to even
+    const int Dk = (D + 1) & ~1, ld = Dk + 1;
+    const int o0 = blockIdx.y * 32, b = blockIdx.z;
+    for (int k = threadIdx.x; k < 32 * Dk; k += kThreads) {
+        const int r = k / Dk, i = k - r * Dk, o = o0 + r;
+        float v = 0.f;
+        if (o < D && i < D) v = transpose ? wgt[(size_t)i * D + o] : wgt[(size_t)o * D + i];
+        sw[r * ld + i] = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 31, h = lane >> 5;
+    const int p = blockIdx.x * 128 + w * 32 + j;
+    const bool pv = p < n;
+    const float* xb = x + (size_t)b * D * n + (pv ? p : 0);
+    f32x16_t acc = {};
+    int k = 0;
+    for (; k + 16 <= Dk; k += 16) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int kk = k + 2 * u + h;
+            av[u] = sw[j * ld + kk];
+            bv[u] = (kk < D && pv) ? xb[(size_t)kk * n] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    for (; k < Dk; k += 2) {
+        const int kk = k + h;
+        const float bv = (kk < D && pv) ? xb[(size_t)kk * n] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[j * ld + kk], bv, acc, 0, 0, 0);
+    }
+    if (!pv) return;
+    float* ob = out + (size_t)b * D * n + p;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int o = o0 + 8 * (e >> 2) + 4 * h + (e & 3);
+        if (o < D) ob[(size_t)o * n] = acc[e];
+    }
+}
+
 int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int radius, int level, int nh, int nw,
                  int extra) {
     RMD_REQUIRE(B > 0 && C > 0 && h > 0 && w > 0 && hl > 0 && wl > 0, RMD_ERR_SHAPE, "rmd_dicl_stack: bad sizes");
@@ -304,6 +533,15 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
                           norm_width, extra_delta);
     if (rc) return rc;
     const int d = 2 * radius + 1;
+    if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
+        dim3 grid((height * width / 4 + kThreads - 1) / kThreads, channels, batch);
+        switch (radius) {
+#define RMD_CASE(RR) case RR: dicl_stack_patch_kernel<RR><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out); break;
+            RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
+#undef RMD_CASE
+        }
+        return check_launch("rmd_dicl_stack/patch");
+    }
     dim3 grid((height * width / 4 + kThreads - 1) / kThreads, d * d, batch);
     dicl_stack_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
     return check_launch("rmd_dicl_stack");
@@ -320,6 +558,16 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
     const int d = 2 * radius + 1;
+    if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
+        (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
+        dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        switch (radius) {
+#define RMD_CASE(RR) case RR: dicl_stack_patch_backward_kernel<RR><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); break;
+            RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
+#undef RMD_CASE
+        }
+        return check_launch("rmd_dicl_stack_backward/patch");
+    }
     dim3 g1((height * width / 4 + kThreads - 1) / kThreads, channels, batch);
     dicl_stack_grad_f1_kernel<<<g1, kThreads, 0, st>>>(grad_stack, P, grad_fmap1);
     (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
@@ -369,6 +617,15 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
                        float* out, void* stream) {
     RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");
     RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap: bad sizes");
+    if (disp <= 1024 && !getenv("RMD_DAP_VALU")) {
+        const int Dk = (disp + 1) & ~1;
+        const size_t lds = sizeof(float) * 32 * (size_t)(Dk + 1);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        dim3 grid((pixels + 127) / 128, (disp + 31) / 32, batch);
+        dap_mfma_kernel<<<grid, kThreads, lds, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
+        return check_launch("rmd_dap/mfma");
+    }
     const size_t lds = sizeof(float) * (size_t)disp * disp;
     dim3 grid((pixels + kThreads - 1) / kThreads, batch);
     if (lds <= 64 * 1024) {

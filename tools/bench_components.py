@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Component benchmark of the non-headline §8 kernels at BASELINE.json's configs (MI355X only).
+
+Times each op with HIP events on its launch stream (median of `reps` launches after warm-up) and
+reports algorithmic HBM bytes per launch, GB/s and the fraction of the 8 TB/s HBM peak:
+  * a6  rmd_dicl_stack        cfg4 (KITTI 384x1280 -> 1/8 level 48x160, C=32, r=4, B=8)
+  * a6' rmd_dicl_stack_backward (same shape)
+  * a8  rmd_dicl_stack_int    cfg3 (DICL 384x512 -> level 2 96x128, C=32, ru=rv=3, B=8)
+  * a9  rmd_dap               cfg4 1/8 level, D=81, B=8 (and D=324 'full')
+  * a11 rmd_corr_lookup_backward + pyramid backward (GEMMs) at cfg5 (FlyingChairs 384x512 -> 48x64,
+        C=256, B=6, 12 lookups)
+  * a4  raft_fs.CorrBlock forward at cfg2 (pyramid with scale 1 + 12 lookups), bf16
+The MatchingNet that consumes a6/a8 (MIOpen convolutions, out of scope) is timed beside them.
+usage: python tools/bench_components.py [reps]   -> one JSON document on stdout
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+import torch  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        ts.append((a, b))
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in ts)
+    return ms[len(ms) // 2]
+
+
+def entry(ms, nbytes, **kw):
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return dict(ms=ms, algorithmic_bytes=nbytes, achieved_GBps=gbs, frac_of_hbm_peak=gbs / PEAK, **kw)
+
+
+def main():
+    import rmd
+    from rmd import ops
+    from rmd.blocks.dicl import MatchingNet
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    res = {}
+
+    def smooth_coords(b, h, w, amp=3.0):
+        """grid + a smooth flow (low-res noise upsampled), as bench.py: the coordinates a flow
+        network produces; per-pixel i.i.d. noise would scatter every gather and atomic."""
+        ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+        low = torch.randn(b, 2, max(h // 8, 2), max(w // 8, 2), generator=g) * amp
+        flow = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=True)
+        return (torch.stack([xs, ys]).float()[None] + flow).to(dev)
+
+    # a6: DICL displacement stack, cfg4 1/8 level
+    b, c, h, w, r = 8, 32, 48, 160, 4
+    f1 = torch.randn(b, c, h, w, generator=g).to(dev)
+    f2 = torch.randn(b, c, h, w, generator=g).to(dev)
+    co = smooth_coords(b, h, w)
+    d = (2 * r + 1) ** 2
+    out_bytes = b * d * 2 * c * h * w * 4
+    res["a6_dicl_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2, co, r), reps),
+                                      out_bytes + 2 * f1.numel() * 4 + co.numel() * 4,
+                                      shape=f"B{b} C{c} {h}x{w} r{r}", output_GB=out_bytes / 1e9)
+    stack = ops.dicl_stack(f1, f2, co, r)
+    gst = torch.randn_like(stack)
+    f1g, f2g = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+
+    def stack_bwd():
+        st = ops.dicl_stack(f1g, f2g, co, r)
+        torch.autograd.grad(st, (f1g, f2g), gst)
+    fwd_ms = res["a6_dicl_stack_cfg4"]["ms"]
+    res["a6_dicl_stack_backward_cfg4"] = entry(max(timed(stack_bwd, reps) - fwd_ms, 1e-6),
+                                               out_bytes + 2 * f1.numel() * 4,
+                                               note="forward+backward time minus forward time")
+    mnet = MatchingNet(2 * c).to(dev).eval()
+    with torch.no_grad():
+        res["a10_matchingnet_cfg4_consumer"] = {"ms": timed(lambda: mnet(stack), max(3, reps // 4)),
+                                                "note": "MIOpen convolutions, out of scope (context)"}
+    del stack, gst
+
+    # a8: DICL integer volume, cfg3 level 2
+    b, c, h, w = 8, 32, 96, 128
+    g1 = torch.randn(b, c, h, w, generator=g).to(dev)
+    g2 = torch.randn(b, c, h, w, generator=g).to(dev)
+    out_bytes = b * 49 * 2 * c * h * w * 4
+    res["a8_dicl_stack_int_cfg3"] = entry(timed(lambda: ops.dicl_stack_int(g1, g2, 3, 3), reps),
+                                          out_bytes + 2 * g1.numel() * 4, shape=f"B{b} C{c} {h}x{w} ru=rv=3",
+                                          output_GB=out_bytes / 1e9)
+
+    # a9: DAP
+    for dd, name in ((81, "a9_dap_d81_cfg4"), (324, "a9_dap_d324_full")):
+        x = torch.randn(8, dd, 48 * 160, generator=g).to(dev)
+        wgt = torch.randn(dd, dd, generator=g).to(dev) / dd
+        res[name] = entry(timed(lambda: ops.dap(x, wgt), reps), 2 * x.numel() * 4 + wgt.numel() * 4,
+                          flop=2.0 * x.numel() * dd)
+
+    # a11: RAFT correlation backward at cfg5 (12 lookups + pyramid backward)
+    b, c, h, w = 6, 256, 48, 64
+    p1 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
+    p2 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
+    cos = [smooth_coords(b, h, w) for _ in range(12)]
+    gos = [torch.randn(b, 324, h, w, generator=g).to(dev) for _ in range(12)]
+
+    def fwd():
+        cb = rmd.raft.CorrBlock(p1, p2, 4, 4, precision="bf16")
+        return sum((cb(cc) * gg).sum() for cc, gg in zip(cos, gos))
+
+    def fwd_bwd():
+        torch.autograd.grad(fwd(), (p1, p2))
+    with torch.no_grad():
+        t_f = timed(lambda: [rmd.raft.CorrBlock(p1.detach(), p2.detach(), 4, 4, precision="bf16")(cc) for cc in cos], reps)
+    t_fb = timed(fwd_bwd, max(3, reps // 2))
+    res["a11_corr_backward_cfg5"] = {"forward_ms": t_f, "forward_backward_ms": t_fb,
+                                     "shape": f"B{b} C{c} {h}x{w}, 12 lookups",
+                                     "note": "forward_backward includes the loss multiply-adds (torch)"}
+
+    # a4: raft_fs block at cfg2
+    b, c, h, w = 8, 256, 55, 128
+    q1 = torch.randn(b, c, h, w, generator=g).to(dev)
+    q2 = torch.randn(b, c, h, w, generator=g).to(dev)
+    cq = smooth_coords(b, h, w)
+    def fs_step():
+        cb = rmd.raft_fs.CorrBlock(q1, q2, 4, 4, precision="bf16")
+        for _ in range(12):
+            cb(cq)
+    with torch.no_grad():
+        res["a4_raft_fs_cfg2_pyramid_plus_12_lookups_bf16"] = {"ms": timed(fs_step, reps)}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
