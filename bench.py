@@ -101,6 +101,23 @@ def cpu_baseline(args, h8, w8):
                       f"pyramid + {args.iters} lookups), oracle/ numpy+BLAS float32, {el:.1f} s"}
 
 
+def job_time(elapsed, world, device):
+    """Whole-job time of the timed region: the MAX over ranks (one all_reduce after the region,
+    nothing on the data path); identity for a single process."""
+    if world <= 1:
+        return elapsed
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    return float(t.item())
+
+
+def rank_inputs(args, rank, h8, w8, device):
+    """Each rank's own batch of frame pairs (weak scaling: per-rank work fixed, seeds differ)."""
+    return synthetic(args.batch, args.channels, h8, w8, args.iters, 1234 + rank, device)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,7 +136,7 @@ def main():
     H, W = padded(args.height, args.width)
     h8, w8 = H // 8, W // 8
     B = args.batch
-    f1, f2, coords = synthetic(B, args.channels, h8, w8, args.iters, 1234 + rank, device)
+    f1, f2, coords = rank_inputs(args, rank, h8, w8, device)
 
     stream = torch.cuda.current_stream(device)
     ev_gemm = []      # (start, end) around the GEMM launch alone (rmd_corr_pyramid_prepared)
@@ -149,11 +166,7 @@ def main():
         step(True)
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-        torch.distributed.barrier()
+    elapsed = job_time(elapsed, world, device)
 
     gemm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_gemm]))
     look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look])) / args.iters

@@ -1,0 +1,130 @@
+"""Multi-process paths.
+
+* Inference shards frame pairs across ranks with no data-path collective; the only exchange is the
+  MAX of the timed region (bench.job_time).  Checked with world_size 2 on `gloo` (CPU).
+* Training: DDP's bucketed gradient all-reduce over the custom autograd of rmd.raft.CorrBlock.
+  Checked on the GPU box with two ranks sharing cuda:0 over `gloo` (the 8-GPU RCCL run is the
+  driver's): DDP-averaged gradients equal the single-process gradient of the concatenated batch.
+"""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _job_time_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+    _init(rank, world, port)
+    try:
+        t = bench.job_time(0.5 + rank, world, torch.device("cpu"))
+        args = argparse.Namespace(batch=2, channels=8, iters=3)
+        f1, _, co = bench.rank_inputs(args, rank, 5, 6, torch.device("cpu"))
+        q.put((rank, t, float(f1.sum()), tuple(co.shape)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_job_time_is_max_over_ranks_and_shards_differ():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_job_time_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [1.5, 1.5]          # both ranks report the slowest rank's time
+    assert res[0][2] != res[1][2]                     # each rank has its own frame pairs
+    assert res[0][3] == (3, 2, 2, 5, 6)
+
+
+class _TinyCorrNet(torch.nn.Module):
+    """1x1-conv 'encoder' -> rmd.raft.CorrBlock -> 2 lookups: parameters get gradients only through
+    the correlation autograd (rmd_corr_lookup_backward + pyramid backward)."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.enc = torch.nn.Conv2d(3, 32, 1)
+        with torch.no_grad():
+            self.enc.weight.copy_(torch.randn(self.enc.weight.shape, generator=g) * 0.3)
+            self.enc.bias.zero_()
+
+    def forward(self, img1, img2, coords):
+        import rmd
+        cb = rmd.raft.CorrBlock(self.enc(img1), self.enc(img2), 2, 2, precision="fp32")
+        return sum(cb(coords + 0.5 * k).square().mean() for k in range(2))
+
+
+def _inputs(b, seed):
+    g = torch.Generator().manual_seed(seed)
+    img1 = torch.randn(b, 3, 12, 16, generator=g)
+    img2 = torch.randn(b, 3, 12, 16, generator=g)
+    ys, xs = torch.meshgrid(torch.arange(12.0), torch.arange(16.0), indexing="ij")
+    co = torch.stack([xs, ys])[None] + torch.randn(b, 2, 12, 16, generator=g)
+    return img1, img2, co
+
+
+def _ddp_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+    _init(rank, world, port)
+    try:
+        dev = torch.device("cuda", 0)
+        net = torch.nn.parallel.DistributedDataParallel(_TinyCorrNet().to(dev))
+        img1, img2, co = (t.to(dev) for t in _inputs(4, 10 + rank))
+        net(img1, img2, co).backward()
+        q.put((rank, net.module.enc.weight.grad.cpu().numpy(), net.module.enc.bias.grad.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ddp_gradient_allreduce_through_corr_autograd():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+    dev = torch.device("cuda", 0)
+    net = _TinyCorrNet().to(dev)
+    loss = 0.0
+    for r in range(2):                 # mean over ranks of each rank's loss == DDP's averaged gradient
+        img1, img2, co = (t.to(dev) for t in _inputs(4, 10 + r))
+        loss = loss + 0.5 * net(img1, img2, co)
+    loss.backward()
+    ref_w = net.enc.weight.grad.cpu().numpy()
+    ref_b = net.enc.bias.grad.cpu().numpy()
+    for _, gw, gb in res:
+        np.testing.assert_allclose(gw, ref_w, rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(gb, ref_b, rtol=1e-4, atol=1e-6)
+    assert np.abs(ref_w).max() > 0
