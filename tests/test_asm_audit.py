@@ -1,4 +1,10 @@
-"""Static audit of the hand-pipelined correlation GEMM (corr_pyramid_stationary) in its gfx950 .s.
+"""Static audit of the correlation GEMM kernels in their gfx950 .s.
+
+corr_pyramid_w8 (the default bf16 path): no scratch, accumulators in VGPRs (no v_accvgpr_read
+round trips), exactly 128 MFMAs and 23 buffer stores per 32-query tile, every store range-checked
+(buffer_store ... offen), the B-fragment loads coalesced global_load_dwordx4.
+
+corr_pyramid_stationary (kept as the RMD_GEMM_KERNEL=stationary A/B reference):
 
 The kernel issues its B-fragment loads in inline asm and retires them with ONE hand-placed
 `s_waitcnt vmcnt(23)`; that is only correct if, between each block of 16 asm loads and its wait,
@@ -17,6 +23,7 @@ import pytest
 from conftest import ROOT
 
 HIPCC = "/opt/rocm/bin/hipcc"
+HIPFLAGS = ["-fno-slp-vectorize"]      # as raft-meets-dicl_amd/csrc/Makefile
 SRC = os.path.join(ROOT, "raft-meets-dicl_amd", "csrc", "corr_pyramid.hip")
 STORES_PER_TILE = {1: 12, 2: 23}      # STraits<TH>::kStores
 
@@ -37,7 +44,7 @@ def module_asm():
     tmp = tempfile.mkdtemp()
     try:
         subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
-                        f"-I{os.path.dirname(SRC)}", "-save-temps", "-c", SRC, "-o", os.path.join(tmp, "x.o")],
+                        f"-I{os.path.dirname(SRC)}", "-save-temps", *HIPFLAGS, "-c", SRC, "-o", os.path.join(tmp, "x.o")],
                        cwd=tmp, check=True, capture_output=True, timeout=600)
         s = [f for f in os.listdir(tmp) if f.endswith(".s") and "gfx950" in f][0]
         txt = open(os.path.join(tmp, s)).read()
@@ -102,3 +109,31 @@ def test_every_asm_load_window_is_exact(kernel_asm):
             assert n == STORES_PER_TILE[th] and stores == STORES_PER_TILE[th], (n, stores)
             windows += 1
     assert windows >= 1, "expected the pipelined load window of the loop"
+
+
+@pytest.fixture
+def w8_asm(module_asm):
+    m = re.search(r"^(_ZN3rmd\w*corr_pyramid_w8ILi2E\w*):[^\n]*\n(.*?)\.end_amdhsa_kernel", module_asm, re.S | re.M)
+    assert m, "corr_pyramid_w8<2> not found"
+    return m.group(2).split("\n")
+
+
+def test_w8_no_scratch_no_agpr_round_trips(w8_asm):
+    body = [ln.strip() for ln in w8_asm]
+    assert not any(ln.startswith("scratch_") for ln in body)
+    assert not any(ln.startswith("v_accvgpr_read") for ln in body)
+
+
+def test_w8_one_tile_per_loop_iteration(w8_asm):
+    """The tile loop holds 128 MFMAs (16 k-steps x 8 target tiles), 16 B-fragment loads and the 23
+    range-checked epilogue stores (16 + 4 + 2 + 1 over levels 0-3)."""
+    body = [ln.strip() for ln in w8_asm]
+    heads = [i for i, ln in enumerate(body) if "Loop Header" in ln]
+    assert heads, "no loop found"
+    start = heads[-1]
+    end = max(i for i, ln in enumerate(body) if ln.startswith("s_cbranch") and i > start)
+    loop = body[start:end]
+    assert sum(ln.startswith("v_mfma_f32_32x32x16_bf16") for ln in loop) == 128
+    assert sum(ln.startswith("global_load_dwordx4") for ln in loop) == 16
+    stores = [ln for ln in loop if ln.startswith("buffer_store")]
+    assert len(stores) == 23 and all(" offen" in ln for ln in stores)
