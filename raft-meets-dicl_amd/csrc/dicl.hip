@@ -16,6 +16,7 @@
 
 #include "rmd_common.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace rmd {
@@ -323,6 +324,70 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
     }
 }
 
+// backward of the general (scaled-grid) stack, raft_dicl_ml levels > 0: every displacement has its
+// own bilinear weights, so each lane (pixel p, channel c) walks the (2r+1)^2 displacements, adds its
+// f1-half gradients into grad_f1 (plain store) and its 4 f2 taps into the workgroup's LDS window
+// (rows [wy0, wy0 + wrows) from the group's lowest tap row; taps past it go to global atomics);
+// the window is then added to grad_f2 once per element.  grid (pixels/256, C, B).
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                                   float* __restrict__ gf1, float* __restrict__ gf2) {
+    __shared__ float win[kWinFloats];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p < n;
+    const int d = 2 * P.radius + 1;
+    float cxs = 0.f, cys = 0.f;
+    if (pv) {
+        cxs = coords[(size_t)b * 2 * n + p] * P.inv_scale;
+        cys = coords[(size_t)b * 2 * n + n + p] * P.inv_scale;
+    }
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    if (pv) {
+        // lowest tap row of this pixel: y of displacement bb = 0 (sy >= 0), clamped into the level
+        const float py = fminf(fmaxf((cys - (float)P.radius) * P.sy, -1.0e6f), 1.0e6f);
+        atomicMin(&wmin, min(max((int)floorf(py), 0), P.hl));
+    }
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    if (pv) {
+        const float* gp = g + (size_t)b * d * d * dstride + p;
+        float s1 = 0.f;
+        for (int a = 0; a < d; ++a) {
+            for (int bb = 0; bb < d; ++bb) {
+                const float* gd = gp + (size_t)(a * d + bb) * dstride;
+                s1 += gd[(size_t)c * n];
+                const float gv = gd[(size_t)(C + c) * n];
+                const float px = (cxs + (float)(a - P.radius)) * P.sx;
+                const float py = (cys + (float)(bb - P.radius)) * P.sy;
+                const Taps t = make_taps(px, py, P.hl, P.wl);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (t.wgt[k] == 0.f) continue;
+                    const int yy = t.idx[k] / P.wl;
+                    float* dst = (yy >= wy0 && yy - wy0 < wrows) ? win + (t.idx[k] - wy0 * P.wl) : g2c + t.idx[k];
+                    atomicAdd(dst, gv * t.wgt[k]);
+                }
+            }
+        }
+        gf1[((size_t)b * C + c) * n + p] = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
+    }
+}
+
 // ---- DICL baseline integer volume ------------------------------------------------------------
 struct IntParams {
     int B, C, h, w, ru, rv;
@@ -568,9 +633,14 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
         }
         return check_launch("rmd_dicl_stack_backward/patch");
     }
+    (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
+    if (level_width <= kWinFloats && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sy >= 0.f) {
+        dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        dicl_stack_general_backward_kernel<<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+        return check_launch("rmd_dicl_stack_backward/general");
+    }
     dim3 g1((height * width / 4 + kThreads - 1) / kThreads, channels, batch);
     dicl_stack_grad_f1_kernel<<<g1, kThreads, 0, st>>>(grad_stack, P, grad_fmap1);
-    (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
     dim3 g2((height * width + kThreads - 1) / kThreads, d * d, batch);
     dicl_stack_grad_f2_kernel<<<g2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap2);
     return check_launch("rmd_dicl_stack_backward");

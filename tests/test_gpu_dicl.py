@@ -164,3 +164,26 @@ def test_dicl_ml_correlation_module_golden(dap_type):
                   _t(g["coords"]), dap=True, mask_costs=g["mask_costs"].tolist())
     assert tuple(out.shape) == g["out"].shape
     assert rel_max_err(out.cpu().numpy(), g["out"]) < 1e-4
+
+
+@pytest.mark.parametrize("level,radius", [(0, 4), (0, 6), (1, 4), (2, 3)])
+def test_dicl_stack_backward_vs_oracle(level, radius):
+    """a6/a7 backward at a cfg4-like size: unit-step patch kernel (level 0, r <= 4), general kernel
+    (r > 4, and raft_dicl_ml levels > 0 whose grid is scaled by (w_l-1)/(w-1)), both with the LDS
+    window.  Oracle: float64 restatement (bilinear scatter)."""
+    import rmd
+    rng = np.random.default_rng(5 + level)
+    b, c, h, w = 2, 16, 24, 80
+    hl, wl = h >> level, w >> level
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, hl, wl)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    co = (np.stack([xs, ys])[None] + rng.normal(0, 2, (b, 2, h, w))).astype(np.float32)
+    t1, t2 = _t(f1, True), _t(f2, True)
+    st = rmd.ops.dicl_stack(t1, t2, _t(co), radius, level=level, norm_hw=(h, w))
+    gst = rng.standard_normal(tuple(st.shape)).astype(np.float32)
+    g1, g2 = torch.autograd.grad(st, (t1, t2), _t(gst))
+    r1, r2 = oracle.dicl_stack_backward(f2.shape, co.astype(np.float64), radius, gst.astype(np.float64),
+                                        level=level, norm_hw=(h, w))
+    assert rel_max_err(g1.cpu().numpy(), r1) < 1e-5
+    assert rel_max_err(g2.cpu().numpy(), r2) < 1e-4

@@ -83,6 +83,20 @@ def main():
     res["a6_dicl_stack_backward_cfg4"] = entry(max(timed(stack_bwd, reps) - fwd_ms, 1e-6),
                                                out_bytes + 2 * f1.numel() * 4,
                                                note="forward+backward time minus forward time")
+    # a7: raft_dicl_ml level 1 (fmap2 at 24x80, grid scaled by (w_l - 1)/(w - 1)): general kernels
+    f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
+    res["a7_dicl_ml_level1_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), reps),
+                                                out_bytes + f1.numel() * 4 + f2l.numel() * 4)
+    stl = ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w))
+    gstl = torch.randn_like(stl)
+    f2lg = f2l.clone().requires_grad_(True)
+
+    def ml_bwd():
+        torch.autograd.grad(ops.dicl_stack(f1g, f2lg, co, r, level=1, norm_hw=(h, w)), (f1g, f2lg), gstl)
+    res["a7_dicl_ml_level1_stack_backward_cfg4"] = entry(
+        max(timed(ml_bwd, reps) - res["a7_dicl_ml_level1_stack_cfg4"]["ms"], 1e-6), out_bytes,
+        note="forward+backward time minus forward time")
+    del stl, gstl
     mnet = MatchingNet(2 * c).to(dev).eval()
     with torch.no_grad():
         res["a10_matchingnet_cfg4_consumer"] = {"ms": timed(lambda: mnet(stack), max(3, reps // 4)),
