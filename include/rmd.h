@@ -108,6 +108,21 @@ int rmd_corr_lookup(const void* pyramid, const rmd_pyramid_desc* desc, const flo
                     int radius, unsigned zero_level_mask, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * On-the-fly windowed correlation (no all-pairs volume).  Replaces raft_fs.CorrBlock
+ * (src/models/impls/raft_fs.py:13-87; scale = 1) and, with levels = 1 and scale = 1/sqrt(C), the
+ * window dot of corr/dot.py:25-57.  rmd_corr_otf_prepare writes the pixel-major query rows
+ * (fmap1 * scale) and the avg-pooled target rows of every level into `workspace`
+ * (rmd_corr_otf_workspace_bytes; compute RMD_F32 = exact f32 MFMA, RMD_BF16 = bf16 MFMA);
+ * rmd_corr_otf_lookup then produces rmd_corr_lookup's output for `coords` from them each iteration.
+ */
+size_t rmd_corr_otf_workspace_bytes(int batch, int channels, int height, int width, int levels, int compute);
+int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int batch, int channels, int height, int width,
+                         int levels, float scale, int compute, void* workspace, void* stream);
+int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int height, int width, int levels,
+                        int compute, const float* coords, int radius, unsigned zero_level_mask, float* out,
+                        void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Backward of the RAFT correlation (training; autograd of raft.py:18-95).  Coordinates are
  * detached in the reference (raft.py:402), so only the feature maps receive gradients.
  *

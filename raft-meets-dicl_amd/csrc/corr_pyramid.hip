@@ -970,8 +970,9 @@ __device__ __forceinline__ bf16x8 lds_frag(const unsigned char* smem, unsigned v
 }
 
 template <int S>
-__device__ __forceinline__ void mma_steps(f32x16 (&acc)[8], const bf16x8 (&bq)[16], bf16x8 (&a)[8],
-                                          const unsigned char* smem, unsigned lane_base, unsigned c) {
+__device__ __forceinline__ void mma_steps(f32x16 (&acc)[8], bf16x8 (&bq)[16], bf16x8 (&a)[8],
+                                          const unsigned char* smem, unsigned lane_base, unsigned c,
+                                          const __bf16* bnext) {
     if constexpr (S < 16) {
         const f32x16 zero = {};
         const unsigned vn = step_addr<(S + 1) & 15>(lane_base, c);
@@ -980,19 +981,22 @@ __device__ __forceinline__ void mma_steps(f32x16 (&acc)[8], const bf16x8 (&bq)[1
             acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ti], bq[S], S == 0 ? zero : acc[ti], 0, 0, 0);
             if constexpr (S + 1 < 16) a[ti] = lds_frag(smem, vn, ti);     // single-buffered: reuse a[ti]
         }
-        mma_steps<S + 1>(acc, bq, a, smem, lane_base, c);
+        // rolling refill: k-step S's B fragment of the NEXT tile loads as soon as this k-step's
+        // MFMAs have consumed the register, a whole tile phase before it is needed
+        if (bnext) bq[S] = *reinterpret_cast<const bf16x8*>(bnext + 512 * S);
+        mma_steps<S + 1>(acc, bq, a, smem, lane_base, c, bnext);
     }
 }
 
-__device__ __forceinline__ void mma(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
-                                    unsigned lane_base, unsigned c) {
+__device__ __forceinline__ void mma(f32x16 (&acc)[8], bf16x8 (&bq)[16], const unsigned char* smem,
+                                    unsigned lane_base, unsigned c, const __bf16* bnext = nullptr) {
     // keep the per-k-step addresses inside the tile loop (hoisted, 16-32 of them would spill)
     asm volatile("" : "+v"(lane_base), "+v"(c));
     bf16x8 a[8];
     const unsigned v0 = step_addr<0>(lane_base, c);
 #pragma unroll
     for (int ti = 0; ti < 8; ++ti) a[ti] = lds_frag(smem, v0, ti);
-    mma_steps<0>(acc, bq, a, smem, lane_base, c);
+    mma_steps<0>(acc, bq, a, smem, lane_base, c, bnext);
 }
 
 template <int S, int AUX>
@@ -1006,10 +1010,10 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx
 
 }  // namespace w8
 
-template <int AUX>
+template <int AUX, bool ROLL>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
-                __half* __restrict__ pyr, int drop_stores) {
+                __half* __restrict__ pyr, int drop_stores, int stagger) {
     constexpr int Cp = 256, CPR = Cp / 8, WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -1079,15 +1083,21 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
 #pragma unroll
         for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 512 * s);
     }
+    if (stagger && w >= 4)           // desynchronise the two waves of each SIMD (diagnostic knob)
+        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
     while (true) {
         f32x16 acc[8];
-        w8::mma(acc, bq, smem, lane_base, lane_c);
         const int qn = qt + stride;
         // next tile's B fragments issue before this tile's stores, so waiting for them never
         // waits for the stores (vmcnt counts in issue order)
         const __bf16* pn = gB + (size_t)min(qn, nqt - 1) * 8192;
+        if constexpr (ROLL) {
+            w8::mma(acc, bq, smem, lane_base, lane_c, pn);
+        } else {
+            w8::mma(acc, bq, smem, lane_base, lane_c);
 #pragma unroll
-        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
+            for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
+        }
         const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
         pipe::EpiState st;
         w8::epilogue<0, AUX>(acc, c, lo, st);
@@ -1168,9 +1178,14 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                 const int aux = aux_env ? atoi(aux_env) : 2;
                 int qs = 1;
                 while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
-                auto kern = aux == 2 ? corr_pyramid_w8<2> : aux == 3 ? corr_pyramid_w8<3> : corr_pyramid_w8<0>;
+                const char* roll_env = getenv("RMD_W8_ROLL");
+                const char* stag_env = getenv("RMD_W8_STAGGER");
+                const bool roll = roll_env && atoi(roll_env);
+                const int stagger = stag_env ? atoi(stag_env) : 0;
+                auto kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true> : corr_pyramid_w8<2, false>)
+                                     : (roll ? corr_pyramid_w8<0, true> : corr_pyramid_w8<0, false>);
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, ab && atoi(ab) == 1);
+                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, ab && atoi(ab) == 1, stagger);
                 return check_launch("rmd_corr_pyramid/gemm-w8");
             }
             if (path == Path::PIPE) {

@@ -129,6 +129,48 @@ def corr_lookup(pyr, coords, radius, mask_costs=()):
     return out
 
 
+# ---- on-the-fly lookup (raft_fs semantics without the volume) -------------------------------------
+
+class OtfState:
+    """Operand rows of rmd_corr_otf_prepare (query rows * scale, pooled target rows of every level)."""
+
+    def __init__(self, ws, b, c, h, w, levels, compute):
+        self.ws, self.b, self.c, self.h, self.w, self.levels, self.compute = ws, b, c, h, w, levels, compute
+
+
+def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
+    _require_gpu(fmap1, fmap2)
+    if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
+        raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
+    compute = PRECISIONS[precision or _default_precision][0]
+    f1 = fmap1.detach().float().contiguous()
+    f2 = fmap2.detach().float().contiguous()
+    b, c, h, w = f1.shape
+    lib = _lib.lib()
+    nbytes = lib.rmd_corr_otf_workspace_bytes(b, c, h, w, levels, compute)
+    if nbytes == 0:
+        raise ValueError(f"otf: unsupported sizes {tuple(f1.shape)} with {levels} levels")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=f1.device)
+    with torch.cuda.device(f1.device):
+        _lib.check(lib.rmd_corr_otf_prepare(_ptr(f1), _ptr(f2), b, c, h, w, levels, float(scale), compute, _ptr(ws),
+                                            _lib.stream_ptr(f1.device)), "rmd_corr_otf_prepare")
+    return OtfState(ws, b, c, h, w, levels, compute)
+
+
+def otf_lookup(st, coords, radius, mask_costs=()):
+    _require_gpu(st.ws, coords)
+    if tuple(coords.shape) != (st.b, 2, st.h, st.w):
+        raise ValueError(f"coords must be (B,2,H,W)=({st.b},2,{st.h},{st.w}), got {tuple(coords.shape)}")
+    co = coords.detach().float().contiguous()
+    dd = (2 * radius + 1) ** 2
+    out = torch.empty((st.b, st.levels * dd, st.h, st.w), dtype=torch.float32, device=co.device)
+    with torch.cuda.device(co.device):
+        _lib.check(_lib.lib().rmd_corr_otf_lookup(_ptr(st.ws), st.b, st.c, st.h, st.w, st.levels, st.compute, _ptr(co),
+                                                  radius, _mask_bits(mask_costs, st.levels), _ptr(out),
+                                                  _lib.stream_ptr(co.device)), "rmd_corr_otf_lookup")
+    return out
+
+
 # ---- RAFT correlation autograd (training) -------------------------------------------------------
 #
 # The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an

@@ -11,7 +11,9 @@ reports algorithmic HBM bytes per launch, GB/s and the fraction of the 8 TB/s HB
         C=256, B=6, 12 lookups)
   * a4  raft_fs.CorrBlock forward at cfg2 (pyramid with scale 1 + 12 lookups), bf16
 The MatchingNet that consumes a6/a8 (MIOpen convolutions, out of scope) is timed beside them.
-usage: python tools/bench_components.py [reps]   -> one JSON document on stdout
+  * f1  on-the-fly lookup (rmd_corr_otf_*) at cfg2: prepare + per-lookup time, bf16 / fp32
+usage: python tools/bench_components.py [reps] [fs]   -> one JSON document on stdout
+      ('fs' runs only the a4 / f1 part)
 """
 import json
 import os
@@ -50,6 +52,7 @@ def main():
     from rmd import ops
     from rmd.blocks.dicl import MatchingNet
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    only = sys.argv[2] if len(sys.argv) > 2 else ""
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     res = {}
@@ -62,82 +65,83 @@ def main():
         flow = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=True)
         return (torch.stack([xs, ys]).float()[None] + flow).to(dev)
 
-    # a6: DICL displacement stack, cfg4 1/8 level
-    b, c, h, w, r = 8, 32, 48, 160, 4
-    f1 = torch.randn(b, c, h, w, generator=g).to(dev)
-    f2 = torch.randn(b, c, h, w, generator=g).to(dev)
-    co = smooth_coords(b, h, w)
-    d = (2 * r + 1) ** 2
-    out_bytes = b * d * 2 * c * h * w * 4
-    res["a6_dicl_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2, co, r), reps),
-                                      out_bytes + 2 * f1.numel() * 4 + co.numel() * 4,
-                                      shape=f"B{b} C{c} {h}x{w} r{r}", output_GB=out_bytes / 1e9)
-    stack = ops.dicl_stack(f1, f2, co, r)
-    gst = torch.randn_like(stack)
-    f1g, f2g = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+    if only != "fs":
+        # a6: DICL displacement stack, cfg4 1/8 level
+        b, c, h, w, r = 8, 32, 48, 160, 4
+        f1 = torch.randn(b, c, h, w, generator=g).to(dev)
+        f2 = torch.randn(b, c, h, w, generator=g).to(dev)
+        co = smooth_coords(b, h, w)
+        d = (2 * r + 1) ** 2
+        out_bytes = b * d * 2 * c * h * w * 4
+        res["a6_dicl_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2, co, r), reps),
+                                          out_bytes + 2 * f1.numel() * 4 + co.numel() * 4,
+                                          shape=f"B{b} C{c} {h}x{w} r{r}", output_GB=out_bytes / 1e9)
+        stack = ops.dicl_stack(f1, f2, co, r)
+        gst = torch.randn_like(stack)
+        f1g, f2g = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
 
-    def stack_bwd():
-        st = ops.dicl_stack(f1g, f2g, co, r)
-        torch.autograd.grad(st, (f1g, f2g), gst)
-    fwd_ms = res["a6_dicl_stack_cfg4"]["ms"]
-    res["a6_dicl_stack_backward_cfg4"] = entry(max(timed(stack_bwd, reps) - fwd_ms, 1e-6),
-                                               out_bytes + 2 * f1.numel() * 4,
-                                               note="forward+backward time minus forward time")
-    # a7: raft_dicl_ml level 1 (fmap2 at 24x80, grid scaled by (w_l - 1)/(w - 1)): general kernels
-    f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
-    res["a7_dicl_ml_level1_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), reps),
-                                                out_bytes + f1.numel() * 4 + f2l.numel() * 4)
-    stl = ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w))
-    gstl = torch.randn_like(stl)
-    f2lg = f2l.clone().requires_grad_(True)
+        def stack_bwd():
+            st = ops.dicl_stack(f1g, f2g, co, r)
+            torch.autograd.grad(st, (f1g, f2g), gst)
+        fwd_ms = res["a6_dicl_stack_cfg4"]["ms"]
+        res["a6_dicl_stack_backward_cfg4"] = entry(max(timed(stack_bwd, reps) - fwd_ms, 1e-6),
+                                                   out_bytes + 2 * f1.numel() * 4,
+                                                   note="forward+backward time minus forward time")
+        # a7: raft_dicl_ml level 1 (fmap2 at 24x80, grid scaled by (w_l - 1)/(w - 1)): general kernels
+        f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
+        res["a7_dicl_ml_level1_stack_cfg4"] = entry(timed(lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), reps),
+                                                    out_bytes + f1.numel() * 4 + f2l.numel() * 4)
+        stl = ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w))
+        gstl = torch.randn_like(stl)
+        f2lg = f2l.clone().requires_grad_(True)
 
-    def ml_bwd():
-        torch.autograd.grad(ops.dicl_stack(f1g, f2lg, co, r, level=1, norm_hw=(h, w)), (f1g, f2lg), gstl)
-    res["a7_dicl_ml_level1_stack_backward_cfg4"] = entry(
-        max(timed(ml_bwd, reps) - res["a7_dicl_ml_level1_stack_cfg4"]["ms"], 1e-6), out_bytes,
-        note="forward+backward time minus forward time")
-    del stl, gstl
-    mnet = MatchingNet(2 * c).to(dev).eval()
-    with torch.no_grad():
-        res["a10_matchingnet_cfg4_consumer"] = {"ms": timed(lambda: mnet(stack), max(3, reps // 4)),
-                                                "note": "MIOpen convolutions, out of scope (context)"}
-    del stack, gst
+        def ml_bwd():
+            torch.autograd.grad(ops.dicl_stack(f1g, f2lg, co, r, level=1, norm_hw=(h, w)), (f1g, f2lg), gstl)
+        res["a7_dicl_ml_level1_stack_backward_cfg4"] = entry(
+            max(timed(ml_bwd, reps) - res["a7_dicl_ml_level1_stack_cfg4"]["ms"], 1e-6), out_bytes,
+            note="forward+backward time minus forward time")
+        del stl, gstl
+        mnet = MatchingNet(2 * c).to(dev).eval()
+        with torch.no_grad():
+            res["a10_matchingnet_cfg4_consumer"] = {"ms": timed(lambda: mnet(stack), max(3, reps // 4)),
+                                                    "note": "MIOpen convolutions, out of scope (context)"}
+        del stack, gst
 
-    # a8: DICL integer volume, cfg3 level 2
-    b, c, h, w = 8, 32, 96, 128
-    g1 = torch.randn(b, c, h, w, generator=g).to(dev)
-    g2 = torch.randn(b, c, h, w, generator=g).to(dev)
-    out_bytes = b * 49 * 2 * c * h * w * 4
-    res["a8_dicl_stack_int_cfg3"] = entry(timed(lambda: ops.dicl_stack_int(g1, g2, 3, 3), reps),
-                                          out_bytes + 2 * g1.numel() * 4, shape=f"B{b} C{c} {h}x{w} ru=rv=3",
-                                          output_GB=out_bytes / 1e9)
+        # a8: DICL integer volume, cfg3 level 2
+        b, c, h, w = 8, 32, 96, 128
+        g1 = torch.randn(b, c, h, w, generator=g).to(dev)
+        g2 = torch.randn(b, c, h, w, generator=g).to(dev)
+        out_bytes = b * 49 * 2 * c * h * w * 4
+        res["a8_dicl_stack_int_cfg3"] = entry(timed(lambda: ops.dicl_stack_int(g1, g2, 3, 3), reps),
+                                              out_bytes + 2 * g1.numel() * 4, shape=f"B{b} C{c} {h}x{w} ru=rv=3",
+                                              output_GB=out_bytes / 1e9)
 
-    # a9: DAP
-    for dd, name in ((81, "a9_dap_d81_cfg4"), (324, "a9_dap_d324_full")):
-        x = torch.randn(8, dd, 48 * 160, generator=g).to(dev)
-        wgt = torch.randn(dd, dd, generator=g).to(dev) / dd
-        res[name] = entry(timed(lambda: ops.dap(x, wgt), reps), 2 * x.numel() * 4 + wgt.numel() * 4,
-                          flop=2.0 * x.numel() * dd)
+        # a9: DAP
+        for dd, name in ((81, "a9_dap_d81_cfg4"), (324, "a9_dap_d324_full")):
+            x = torch.randn(8, dd, 48 * 160, generator=g).to(dev)
+            wgt = torch.randn(dd, dd, generator=g).to(dev) / dd
+            res[name] = entry(timed(lambda: ops.dap(x, wgt), reps), 2 * x.numel() * 4 + wgt.numel() * 4,
+                              flop=2.0 * x.numel() * dd)
 
-    # a11: RAFT correlation backward at cfg5 (12 lookups + pyramid backward)
-    b, c, h, w = 6, 256, 48, 64
-    p1 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
-    p2 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
-    cos = [smooth_coords(b, h, w) for _ in range(12)]
-    gos = [torch.randn(b, 324, h, w, generator=g).to(dev) for _ in range(12)]
+        # a11: RAFT correlation backward at cfg5 (12 lookups + pyramid backward)
+        b, c, h, w = 6, 256, 48, 64
+        p1 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
+        p2 = torch.randn(b, c, h, w, generator=g).to(dev).requires_grad_(True)
+        cos = [smooth_coords(b, h, w) for _ in range(12)]
+        gos = [torch.randn(b, 324, h, w, generator=g).to(dev) for _ in range(12)]
 
-    def fwd():
-        cb = rmd.raft.CorrBlock(p1, p2, 4, 4, precision="bf16")
-        return sum((cb(cc) * gg).sum() for cc, gg in zip(cos, gos))
+        def fwd():
+            cb = rmd.raft.CorrBlock(p1, p2, 4, 4, precision="bf16")
+            return sum((cb(cc) * gg).sum() for cc, gg in zip(cos, gos))
 
-    def fwd_bwd():
-        torch.autograd.grad(fwd(), (p1, p2))
-    with torch.no_grad():
-        t_f = timed(lambda: [rmd.raft.CorrBlock(p1.detach(), p2.detach(), 4, 4, precision="bf16")(cc) for cc in cos], reps)
-    t_fb = timed(fwd_bwd, max(3, reps // 2))
-    res["a11_corr_backward_cfg5"] = {"forward_ms": t_f, "forward_backward_ms": t_fb,
-                                     "shape": f"B{b} C{c} {h}x{w}, 12 lookups",
-                                     "note": "forward_backward includes the loss multiply-adds (torch)"}
+        def fwd_bwd():
+            torch.autograd.grad(fwd(), (p1, p2))
+        with torch.no_grad():
+            t_f = timed(lambda: [rmd.raft.CorrBlock(p1.detach(), p2.detach(), 4, 4, precision="bf16")(cc) for cc in cos], reps)
+        t_fb = timed(fwd_bwd, max(3, reps // 2))
+        res["a11_corr_backward_cfg5"] = {"forward_ms": t_f, "forward_backward_ms": t_fb,
+                                         "shape": f"B{b} C{c} {h}x{w}, 12 lookups",
+                                         "note": "forward_backward includes the loss multiply-adds (torch)"}
 
     # a4: raft_fs block at cfg2
     b, c, h, w = 8, 256, 55, 128
@@ -150,6 +154,19 @@ def main():
             cb(cq)
     with torch.no_grad():
         res["a4_raft_fs_cfg2_pyramid_plus_12_lookups_bf16"] = {"ms": timed(fs_step, reps)}
+        # f1: on-the-fly lookup (no volume), bf16 and exact-f32 MFMA
+        for prec in ("bf16", "fp32"):
+            st = ops.otf_prepare(q1, q2, 4, prec)
+            t_prep = timed(lambda: ops.otf_prepare(q1, q2, 4, prec), reps)
+            t_look = timed(lambda: ops.otf_lookup(st, cq, 4), reps)
+            es = 2 if prec == "bf16" else 4
+            rows = b * (h * w + sum((h >> l) * (w >> l) for l in range(4))) * c * es
+            out_b = b * 4 * 81 * h * w * 4
+            res[f"f1_otf_cfg2_{prec}"] = dict(
+                prepare_ms=t_prep, lookup_ms=t_look, step_12_lookups_ms=t_prep + 12 * t_look,
+                lookup_algorithmic_bytes=rows + out_b + cq.numel() * 4,
+                lookup_GBps=(rows + out_b + cq.numel() * 4) / (t_look * 1e-3) / 1e9,
+                workspace_MB=st.ws.numel() / 1e6)
     print(json.dumps(res, indent=1))
 
 

@@ -23,30 +23,44 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     dev = torch.device("cuda", 0)
     f1, f2, _ = bench.synthetic(8, 256, 55, 128, 1, 1234, dev)
+    names = os.environ.get("RMD_AB", "w8,stationary").split(",")
+    rounds = int(os.environ.get("RMD_AB_ROUNDS", "5"))
+    times = {n: [] for n in names}
     res, ref = {}, None
-    for name in os.environ.get("RMD_AB", "pipe,stationary").split(","):
+
+    def configure(name):
         kern, _, abl = name.partition(":")          # e.g. "pipe:1" = RMD_ABLATE=1 (stores dropped)
         kern, _, aux = kern.partition("@")          # e.g. "w8@2" = RMD_STORE_AUX=2
+        kern, _, knobs = kern.partition("+")        # e.g. "w8+roll+stag4" = RMD_W8_ROLL=1, RMD_W8_STAGGER=4
+        os.environ["RMD_W8_ROLL"] = "1" if "roll" in knobs else "0"
+        os.environ["RMD_W8_STAGGER"] = knobs.split("stag")[1].split("+")[0] if "stag" in knobs else "0"
         os.environ["RMD_GEMM_KERNEL"] = kern
         os.environ["RMD_ABLATE"] = abl or "0"
         os.environ["RMD_STORE_AUX"] = aux or "2"
-        ev = []
-        for _ in range(3):
-            pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
-        torch.cuda.synchronize()
-        for _ in range(reps):
-            pyr = ops.corr_pyramid(f1, f2, 4, "bf16", events=ev)
-        torch.cuda.synchronize()
-        ms = sorted(a.elapsed_time(b) for a, b in ev)
-        res[name] = {"median_ms": ms[len(ms) // 2], "min_ms": ms[0],
-                     "write_TBps": pyr.data.numel() * 2 / (ms[len(ms) // 2] * 1e-3) / 1e12}
-        if abl:
-            continue
-        if ref is None:
-            ref = pyr.data.clone()
-        else:
-            diff = (pyr.data.view(torch.int16) != ref.view(torch.int16)).sum().item()
-            res[name]["bitwise_mismatch_vs_first"] = int(diff)
+        return abl
+
+    for _ in range(5):                              # chip warm-up (clocks) before any timed variant
+        ops.corr_pyramid(f1, f2, 4, "bf16")
+    for rnd in range(rounds):                       # variants interleaved round by round
+        for name in names:
+            abl = configure(name)
+            ev = []
+            for _ in range(2):
+                pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
+            for _ in range(reps):
+                pyr = ops.corr_pyramid(f1, f2, 4, "bf16", events=ev)
+            torch.cuda.synchronize()
+            times[name] += [a.elapsed_time(b) for a, b in ev]
+            if rnd == 0 and not abl:
+                if ref is None:
+                    ref = pyr.data.clone()
+                else:
+                    res.setdefault(name, {})["bitwise_mismatch_vs_first"] = int(
+                        (pyr.data.view(torch.int16) != ref.view(torch.int16)).sum().item())
+    for name in names:
+        ms = sorted(times[name])
+        res.setdefault(name, {}).update(median_ms=ms[len(ms) // 2], min_ms=ms[0],
+                                        write_TBps=pyr.data.numel() * 2 / (ms[len(ms) // 2] * 1e-3) / 1e12)
     print(json.dumps(res, indent=1))
 
 

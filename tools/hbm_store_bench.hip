@@ -67,7 +67,7 @@ __global__ void seq_store2(uint4* p, long long n16) {
 // blocked layout: one record of 340 targets x 32 queries (fp16) per (block, 32-query tile); the
 // WAVES waves of a workgroup write records qt = w, w+WAVES, ... of their block, store by store:
 // 16 + 4 x 1 KiB, 2 x 512 B (8 B/lane), 1 x 256 B (4 B/lane)
-template <int WAVES, bool NT>
+template <int WAVES, bool NT, bool QTMAJOR = false>
 __global__ void __launch_bounds__(512) blocked_store(unsigned char* pyr, int nblk_total, int nqt) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(512) blocked_store(unsigned char* pyr, int nbl
     if (w >= WAVES) return;
     const u4 v = {(unsigned)lane, 1u, 2u, 3u};
     for (int qt = w; qt < nqt; qt += WAVES) {
-        unsigned char* rec = pyr + ((size_t)blk * nqt + qt) * 21760;
+        unsigned char* rec = QTMAJOR ? pyr + ((size_t)qt * nblk_total + blk) * 21760 : pyr + ((size_t)blk * nqt + qt) * 21760;
         for (int k = 0; k < 20; ++k) {
             u4* p = reinterpret_cast<u4*>(rec + k * 1024) + lane;
             if (NT) __builtin_nontemporal_store(v, p); else *p = v;
@@ -176,6 +176,9 @@ int main() {
         timeit("blocked_w8", [&] { blocked_store<8, false><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
         timeit("blocked_w8_nt", [&] { blocked_store<8, true><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
         timeit("blocked_w4", [&] { blocked_store<4, false><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
+        timeit("blocked_w8_qtmajor", [&] { blocked_store<8, false, true><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
+        timeit("blocked_w8_qtmajor_nt", [&] { blocked_store<8, true, true><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
+        timeit("blocked_w8_again", [&] { blocked_store<8, false><<<nb, 512>>>(reinterpret_cast<unsigned char*>(pyr), nb, nqt); });
     }
     timeit("seq", [&] { seq_store<<<4096, 256>>>(reinterpret_cast<uint4*>(pyr), (long long)(bytes / 16)); });
     timeit("gemm", [&] { gemm_store<0, 32><<<B * nblk, 256>>>(pyr, g); });
