@@ -5,120 +5,187 @@
 // and, with one level and scale 1/sqrt(C), the window dot of corr/dot.py:25-57.  SURVEY.md §8(f)
 // rank 1: memory O(B*C*N) instead of O(B*N^2).
 //
-// Per launch: grid (query blocks of 16 x 2 pixels, levels, batch), 256 threads.  The 32 queries'
-// (2r+2)^2 integer patches at level l are bounded by one box (clipped to the level map); if it has
-// at most kMaxT targets, S = targets x queries is one dense MFMA product (bf16 32x32x16, or exact
-// f32 32x32x2) into LDS, target rows gathered from the pooled pixel-major fmap2 (rmd_corr_otf_prepare)
-// and query fragments from the pixel-major fmap1.  Every query then interpolates its window from
-// LDS exactly as rmd_corr_lookup does (shared bilinear weights, zero padding per tap, NaN for
-// 1-pixel levels, zeroed masked levels).  A box larger than kMaxT (pathological flow spread) falls
-// back to per-query patch dots on the VALU.
+// Operand layout (rmd_corr_otf_prepare): every map row is cut into segments of 16 pixels; a segment
+// holds Cp channels of its 16 pixels as Cp/LSC load steps of exactly the 1 KiB one wave-instruction
+// loads (16 B per lane), already in the lane order of the 16x16 MFMA operand (lane = 16*g + pixel):
+//   bf16  16x16x32: lane (g, i) holds channels 32*ls + 8*g + e, e < 8           (one MFMA per step)
+//   f32   16x16x4 : lane (g, i) holds channels 16*ls + 4*m + g, m < 4           (four MFMAs per step)
+// so operand loads are whole 128-B lines (the row-per-lane gather of a pixel-major layout touches 32
+// lines per instruction and halves the L1 rate).  Query rows (fmap1 * scale) use the same layout.
+//
+// Lookup: one 256-thread block per (16 x 2 query block, level, batch).  The 32 queries' (2r+2)^2
+// integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
+// processed in bands of whole rows of at most kMaxT targets: S = band targets x queries, one 16x16
+// MFMA tile per (target segment, query segment), into LDS.  Each (query, x-offset) thread keeps its
+// window rows x-interpolated in registers across bands and finally y-interpolates exactly as
+// rmd_corr_lookup does (shared bilinear weights, zero padding per tap, NaN for 1-pixel levels, zeroed
+// masked levels).  A box wider than kMaxT (flow differing by hundreds of pixels inside one block)
+// takes a per-query VALU patch path.
 #include "rmd_common.h"
 
 namespace rmd {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kBX = 16, kBY = 2, kQ = kBX * kBY;     // query block
-constexpr int kMaxT = 512;                            // LDS: kQ x kMaxT f32 = 64 KiB
-constexpr int kCp = 32;                               // channel padding of the operand rows
+constexpr int kThreads = 256;                        // prepare kernels
+constexpr int kLookThreads = 256, kWaves = kLookThreads / 64;
+constexpr int kBX = 16, kBY = 2, kQ = kBX * kBY;     // query block = 2 query segments
+constexpr int kMaxT = 384;                           // targets of one band
+constexpr int kLd = kMaxT + 5;                       // S row stride (spreads queries over banks)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+template <typename T> struct Seg;
+template <> struct Seg<__bf16> {
+    static constexpr int LE = 8, LSC = 32;           // elements per lane, channels per load step
+    typedef bf16x8 frag;
+    static __device__ __forceinline__ void mma(f32x4& acc, const frag& a, const frag& b) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    }
+    // (lane, element) of channel c within a load step
+    static __host__ __device__ constexpr int lane_g(int c) { return (c >> 3) & 3; }
+    static __host__ __device__ constexpr int elem(int c) { return c & 7; }
+};
+template <> struct Seg<float> {
+    static constexpr int LE = 4, LSC = 16;
+    typedef f32x4 frag;
+    static __device__ __forceinline__ void mma(f32x4& acc, const frag& a, const frag& b) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], b[m], acc, 0, 0, 0);
+    }
+    static __host__ __device__ constexpr int lane_g(int c) { return c & 3; }
+    static __host__ __device__ constexpr int elem(int c) { return (c >> 2) & 3; }
+};
 
 struct OtfGeom {
     int B, C, Cp, H, W, L;
-    int lh[RMD_MAX_LEVELS], lw[RMD_MAX_LEVELS];
-    long long toff[RMD_MAX_LEVELS], T;
+    int lh[RMD_MAX_LEVELS], lw[RMD_MAX_LEVELS], nsx[RMD_MAX_LEVELS];
+    long long soff[RMD_MAX_LEVELS], TS;               // target segments: level offsets, per batch
+    int qnsx;
+    long long QS;                                     // query segments per batch
 };
+
+// operand channel padding: one of the compiled channel counts, else a multiple of 128
+int otf_cp(int C) {
+    for (int c : {32, 64, 128, 256})
+        if (C <= c) return c;
+    return (C + 127) / 128 * 128;
+}
 
 OtfGeom make_otf_geom(int B, int C, int H, int W, int L) {
     OtfGeom g{};
     g.B = B;
     g.C = C;
-    g.Cp = (C + kCp - 1) / kCp * kCp;
+    g.Cp = otf_cp(C);
     g.H = H;
     g.W = W;
     g.L = L;
-    long long t = 0;
+    long long s = 0;
     for (int l = 0; l < L; ++l) {
         g.lh[l] = H >> l;
         g.lw[l] = W >> l;
-        g.toff[l] = t;
-        t += (long long)g.lh[l] * g.lw[l];
+        g.nsx[l] = (g.lw[l] + 15) / 16;
+        g.soff[l] = s;
+        s += (long long)g.lh[l] * g.nsx[l];
     }
-    g.T = t;
+    g.TS = s;
+    g.qnsx = (W + 15) / 16;
+    g.QS = (long long)H * g.qnsx;
     return g;
 }
 
-template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+// workspace: query segments (B, QS) | target segments (B, TS) | f32 scratch of levels 1.. (B, C, lh, lw)
+size_t otf_query_elems(const OtfGeom& g) { return (size_t)g.B * g.QS * 16 * g.Cp; }
+size_t otf_scratch_elems(const OtfGeom& g) {
+    size_t n = 0;
+    for (int l = 1; l < g.L; ++l) n += (size_t)g.B * g.C * g.lh[l] * g.lw[l];
+    return n;
+}
+size_t otf_scratch_offset(const OtfGeom& g, size_t es) {
+    return ((size_t)g.B * (g.QS + g.TS) * 16 * g.Cp * es + 255) / 256 * 256;
+}
 
-// rows[b][t][c] = scale * mean over the 2^l x 2^l block of f[b][c][...] (level l of target t), in the
-// compute type, channels zero-padded to Cp.  levels = 1, scale = s gives the query operand.
+// Level l of fmap2 as the reference builds it (raft_fs.py:27-30): F.avg_pool2d(k=2, s=2) of level l-1.
+// src / dst are (B, C, h, w) / (B, C, h/2, w/2) float32; one thread per output element.
+__global__ void __launch_bounds__(kThreads)
+otf_pool2_kernel(const float* __restrict__ src, int BC, int h, int w, float* __restrict__ dst) {
+    const int h2 = h >> 1, w2 = w >> 1;
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= (long long)BC * h2 * w2) return;
+    const int x = (int)(idx % w2);
+    const long long r = idx / w2;
+    const int y = (int)(r % h2);
+    const long long bc = r / h2;
+    const float* p = src + (size_t)bc * h * w + (size_t)(2 * y) * w + 2 * x;
+    dst[idx] = (p[0] + p[1] + p[w] + p[w + 1]) * 0.25f;
+}
+
+struct LevelSrc {
+    const float* p[RMD_MAX_LEVELS];      // (B, C, lh, lw) float32 per level
+};
+
+// Segment operands: one thread per 16-B lane chunk (segment, load step, lane); a wave writes one
+// contiguous 1-KiB load step, its reads run along x within each channel.
+// levels = 1 and scale = s give the query operand (fmap1 * s).
 template <typename T>
 __global__ void __launch_bounds__(kThreads)
-otf_rows_kernel(const float* __restrict__ f, OtfGeom g, float scale, T* __restrict__ rows) {
+otf_segments_kernel(LevelSrc src, OtfGeom g, float scale, T* __restrict__ seg) {
+    using S = Seg<T>;
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const int CG = g.Cp / 8;
-    const long long total = (long long)g.B * g.T * CG;
+    const int nls = g.Cp / S::LSC;
+    const long long total = (long long)g.B * g.TS * nls * 64;
     if (idx >= total) return;
-    const int cg = (int)(idx % CG);
-    const long long bt = idx / CG;
-    const long long t = bt % g.T;
-    const int b = (int)(bt / g.T);
+    const int lane = (int)(idx & 63), gq = lane >> 4, i = lane & 15;
+    const long long r = idx >> 6;
+    const int ls = (int)(r % nls);
+    const long long bs = r / nls;
+    const long long s = bs % g.TS;
+    const int b = (int)(bs / g.TS);
     int l = 0;
 #pragma unroll
     for (int k = 1; k < RMD_MAX_LEVELS; ++k)
-        if (k < g.L && t >= g.toff[k]) l = k;
-    const int tl = (int)(t - g.toff[l]);
-    const int y = tl / g.lw[l], x = tl - y * g.lw[l];
-    const int s = 1 << l;
-    T out[8];
+        if (k < g.L && s >= g.soff[k]) l = k;
+    const int sl = (int)(s - g.soff[l]);
+    const int y = sl / g.nsx[l], x = (sl - y * g.nsx[l]) * 16 + i;
+    const size_t plane = (size_t)g.lh[l] * g.lw[l];
+    const float* base = src.p[l] + (size_t)b * g.C * plane + (size_t)y * g.lw[l] + x;
+    typedef __attribute__((ext_vector_type(S::LE))) T frag_t;
+    frag_t v;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int c = cg * 8 + e;
-        float acc = 0.f;
-        if (c < g.C) {
-            const float* src = f + ((size_t)b * g.C + c) * g.H * g.W + (size_t)(y * s) * g.W + x * s;
-            for (int dy = 0; dy < s; ++dy)
-                for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.W + dx];
-            acc *= scale / (float)(s * s);
-        }
-        out[e] = from_f32<T>(acc);
+    for (int e = 0; e < S::LE; ++e) {
+        // channel of element e of lane group gq (inverse of Seg::lane_g / Seg::elem)
+        const int c = S::LE == 8 ? ls * 32 + gq * 8 + e : ls * 16 + 4 * e + gq;
+        v[e] = (T)(x < g.lw[l] && c < g.C ? base[(size_t)c * plane] * scale : 0.f);
     }
-    T* dst = rows + ((size_t)b * g.T + t) * g.Cp + cg * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dst[e] = out[e];
+    *reinterpret_cast<frag_t*>(seg + (size_t)idx * S::LE) = v;
 }
 
-template <typename T> struct Mfma;
-template <> struct Mfma<__bf16> {
-    static constexpr int KS = 16;        // k per MFMA
-    static __device__ __forceinline__ void step(f32x16& acc, const __bf16* a, const __bf16* b) {
-        const bf16x8 av = *reinterpret_cast<const bf16x8*>(a);
-        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(b);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
-    }
-    static constexpr int lane_k(int h) { return 8 * h; }
-};
-template <> struct Mfma<float> {
-    static constexpr int KS = 2;
-    static __device__ __forceinline__ void step(f32x16& acc, const float* a, const float* b) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(*a, *b, acc, 0, 0, 0);
-    }
-    static constexpr int lane_k(int h) { return h; }
-};
+// element (pixel i of segment, channel c) of a segment operand
+template <typename T>
+__device__ __forceinline__ float seg_elem(const T* segbase, int i, int c) {
+    using S = Seg<T>;
+    return (float)segbase[(c / S::LSC) * 64 * S::LE + (S::lane_g(c) * 16 + i) * S::LE + S::elem(c)];
+}
 
-template <typename T, int R>
-__global__ void __launch_bounds__(kThreads)
-otf_lookup_kernel(const T* __restrict__ qrows, const T* __restrict__ trows, OtfGeom g,
+// 1-D grid over (batch, level, query block), XCD-aware: adjacent query blocks, whose target boxes
+// overlap, run on the same XCD and share its L2.  CPT = compiled Cp (0: runtime multiple of 128).
+template <typename T, int R, int CPT>
+__global__ void __launch_bounds__(kLookThreads)
+otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
+    using SG = Seg<T>;
+    using frag = typename SG::frag;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K;
-    extern __shared__ float S[];                       // [kQ][kMaxT] (box) or [kQ][KK] (per query)
+    extern __shared__ float S[];                       // [kQ][kLd]: band (boxed) or patch (per query)
     __shared__ int box[4];                             // x0, x1, y0, y1 (min / max)
-    const int nbx = (g.W + kBX - 1) / kBX;
-    const int qx0 = (blockIdx.x % nbx) * kBX, qy0 = (blockIdx.x / nbx) * kBY;
-    const int L = blockIdx.y, b = blockIdx.z;
+    __shared__ int sxs[kQ], sys[kQ];
+    __shared__ float sfx[kQ], sfy[kQ];
+    const int nbx = (g.W + kBX - 1) / kBX, nqb = nbx * ((g.H + kBY - 1) / kBY);
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+    const int qb = lid % nqb, L = (lid / nqb) % g.L, b = lid / (nqb * g.L);
+    const int qx0 = (qb % nbx) * kBX, qy0 = (qb / nbx) * kBY;
     const int N = g.H * g.W;
     const int lh = g.lh[L], lw = g.lw[L];
     const int tid = threadIdx.x;
@@ -128,7 +195,7 @@ otf_lookup_kernel(const T* __restrict__ qrows, const T* __restrict__ trows, OtfG
     const bool masked = (zmask >> L) & 1u;
     if (masked || lh < 2 || lw < 2) {
         const float v = masked ? 0.f : __builtin_nanf("");
-        for (int idx = tid; idx < kQ * D * D; idx += kThreads) {
+        for (int idx = tid; idx < kQ * D * D; idx += kLookThreads) {
             const int q = idx % kQ, c = idx / kQ;
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y < g.H && x < g.W) ob[(size_t)c * N + y * g.W + x] = v;
@@ -136,20 +203,6 @@ otf_lookup_kernel(const T* __restrict__ qrows, const T* __restrict__ trows, OtfG
         return;
     }
 
-    // per-query patch origin at level L
-    auto origin = [&](int q, int& xs, int& ys, float& fx, float& fy) {
-        const int y = min(qy0 + q / kBX, g.H - 1), x = min(qx0 + q % kBX, g.W - 1);
-        const float inv = 1.0f / (float)(1 << L);
-        float cx = coords[((size_t)b * 2 + 0) * N + y * g.W + x] * inv;
-        float cy = coords[((size_t)b * 2 + 1) * N + y * g.W + x] * inv;
-        cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
-        cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
-        const float fx0 = floorf(cx), fy0 = floorf(cy);
-        fx = cx - fx0;
-        fy = cy - fy0;
-        xs = (int)fx0 - R;
-        ys = (int)fy0 - R;
-    };
     if (tid == 0) {
         box[0] = 1 << 30;
         box[1] = -(1 << 30);
@@ -158,9 +211,19 @@ otf_lookup_kernel(const T* __restrict__ qrows, const T* __restrict__ trows, OtfG
     }
     __syncthreads();
     if (tid < kQ) {
-        int xs, ys;
-        float fx, fy;
-        origin(tid, xs, ys, fx, fy);
+        // query's window origin at level L (coords clamped as rmd_corr_lookup does)
+        const int y = min(qy0 + tid / kBX, g.H - 1), x = min(qx0 + tid % kBX, g.W - 1);
+        const float inv = 1.0f / (float)(1 << L);
+        float cx = coords[((size_t)b * 2 + 0) * N + y * g.W + x] * inv;
+        float cy = coords[((size_t)b * 2 + 1) * N + y * g.W + x] * inv;
+        cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+        cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+        const float fx0 = floorf(cx), fy0 = floorf(cy);
+        const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+        sxs[tid] = xs;
+        sys[tid] = ys;
+        sfx[tid] = cx - fx0;
+        sfy[tid] = cy - fy0;
         atomicMin(&box[0], xs);
         atomicMax(&box[1], xs + K - 1);
         atomicMin(&box[2], ys);
@@ -169,76 +232,131 @@ otf_lookup_kernel(const T* __restrict__ qrows, const T* __restrict__ trows, OtfG
     __syncthreads();
     const int bx0 = max(box[0], 0), bx1 = min(box[1], lw - 1);
     const int by0 = max(box[2], 0), by1 = min(box[3], lh - 1);
-    const int tw = max(bx1 - bx0 + 1, 0), th = max(by1 - by0 + 1, 0);
-    const int tb = tw * th;
-    const bool dense = tb <= kMaxT;
-    const T* qb = qrows + (size_t)b * N * g.Cp;
-    const T* tl = trows + ((size_t)b * g.T + g.toff[L]) * g.Cp;
+    const int th = max(by1 - by0 + 1, 0);
+    const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0, sw = nseg * 16;
+    const int cp = CPT > 0 ? CPT : g.Cp;
+    const int nls = cp / SG::LSC;
+    const size_t segsz = (size_t)16 * cp;
+    const T* qsb = qseg + ((size_t)b * g.QS + (size_t)qy0 * g.qnsx + (qx0 >> 4)) * segsz;
+    const T* qsb1 = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + 1, g.H - 1) * g.qnsx + (qx0 >> 4)) * segsz;
+    const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
 
-    if (dense && tb > 0) {
-        // S[q][t] for the box's targets: 32-target MFMA tiles spread over the 4 waves
-        const int lane = tid & 63, w = tid >> 6, j = lane & 31, h = lane >> 5;
-        const int qy = min(qy0 + j / kBX, g.H - 1), qx = min(qx0 + j % kBX, g.W - 1);
-        const T* qrow = qb + (size_t)(qy * g.W + qx) * g.Cp + Mfma<T>::lane_k(h);
-        const int ntile = (tb + 31) / 32;
-        for (int tile = w; tile < ntile; tile += 4) {
-            const int t = min(tile * 32 + j, tb - 1);
-            const int ty = by0 + t / tw, tx = bx0 + t % tw;
-            const T* trow = tl + (size_t)(ty * lw + tx) * g.Cp + Mfma<T>::lane_k(h);
-            f32x16 acc = {};
-            for (int k = 0; k < g.Cp; k += Mfma<T>::KS) Mfma<T>::step(acc, trow + k, qrow + k);
+    // thread items (q, a): query q, window x-offset a; hx[i][jj] = row jj of the window, x-interpolated
+    constexpr int ITEMS = (kQ * D + kLookThreads - 1) / kLookThreads;
+    float hx[ITEMS][K];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int tt = tile * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
-                if (tt < tb) S[j * kMaxT + tt] = acc[e];
+    for (int i = 0; i < ITEMS; ++i)
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
+
+    if (sw <= kMaxT) {
+        const int lane = tid & 63, w = tid >> 6;
+        const int bh = sw > 0 ? kMaxT / sw : 1;
+        // the block's two query segments, held in registers for every target segment (CPT > 0)
+        constexpr int NLS = CPT > 0 ? CPT / SG::LSC : 1;
+        frag q0[NLS], q1[NLS];
+        if constexpr (CPT > 0) {
+#pragma unroll
+            for (int ls = 0; ls < NLS; ++ls) {
+                q0[ls] = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
+                q1[ls] = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
             }
         }
-    } else if (!dense) {
-        // fallback: each query's own (2r+2)^2 patch, one dot product per thread
-        for (int idx = tid; idx < kQ * KK; idx += kThreads) {
+        for (int ry0 = by0; ry0 < by0 + th; ry0 += bh) {
+            const int nrow = min(bh, by0 + th - ry0), ntask = nrow * nseg;
+            for (int task = w; task < ntask; task += kWaves) {
+                const int trow = ry0 + task / nseg, ts = task % nseg;
+                const T* tsb = tlev + ((size_t)trow * g.nsx[L] + sa + ts) * segsz + (size_t)lane * SG::LE;
+                f32x4 a0 = {}, a1 = {};
+                if constexpr (CPT > 0) {
+                    frag t[NLS];
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) {
+                        SG::mma(a0, t[ls], q0[ls]);
+                        SG::mma(a1, t[ls], q1[ls]);
+                    }
+                } else {
+                    for (int ls = 0; ls < nls; ++ls) {
+                        const frag t = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                        const frag u0 = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
+                        const frag u1 = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
+                        SG::mma(a0, t, u0);
+                        SG::mma(a1, t, u1);
+                    }
+                }
+                // C[target 4*(lane>>4)+e][query lane&15] -> S[query][band target]
+                const int col = (trow - ry0) * sw + ts * 16 + 4 * (lane >> 4), j = lane & 15;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    S[j * kLd + col + e] = a0[e];
+                    S[(16 + j) * kLd + col + e] = a1[e];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const int idx = tid + i * kLookThreads;
+                if (idx >= kQ * D) break;
+                const int q = idx % kQ, a = idx / kQ;
+                const int xs = sxs[q], ys = sys[q];
+                const float fx = sfx[q];
+                const float* Sq = S + q * kLd;
+#pragma unroll
+                for (int jj = 0; jj < K; ++jj) {
+                    const int ty = ys + jj;
+                    if (ty >= ry0 && ty < ry0 + nrow) {
+                        float v[2];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const int tx = xs + a + u;
+                            v[u] = (tx >= 0 && tx < lw) ? Sq[(ty - ry0) * sw + (tx - sa * 16)] : 0.f;
+                        }
+                        hx[i][jj] = fmaf(fx, v[1] - v[0], v[0]);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        // box wider than kMaxT: each query's own (2r+2)^2 patch, one dot product per thread
+        for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
             const int q = idx / KK, r = idx - q * KK;
-            int xs, ys;
-            float fx, fy;
-            origin(q, xs, ys, fx, fy);
-            const int ty = ys + r / K, tx = xs + r % K;
+            const int ty = sys[q] + r / K, tx = sxs[q] + r % K;
             float acc = 0.f;
             if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
-                const int qy = min(qy0 + q / kBX, g.H - 1), qx = min(qx0 + q % kBX, g.W - 1);
-                const T* qrow = qb + (size_t)(qy * g.W + qx) * g.Cp;
-                const T* trow = tl + (size_t)(ty * lw + tx) * g.Cp;
-                for (int c = 0; c < g.C; ++c) acc = fmaf((float)qrow[c], (float)trow[c], acc);
+                const T* qs = q < kBX ? qsb : qsb1;
+                const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
+                for (int c = 0; c < g.C; ++c) acc = fmaf(seg_elem(qs, q % kBX, c), seg_elem(ts, tx & 15, c), acc);
             }
-            S[q * KK + r] = acc;
+            S[q * kLd + r] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const int idx = tid + i * kLookThreads;
+            if (idx >= kQ * D) break;
+            const int q = idx % kQ, a = idx / kQ;
+            const float fx = sfx[q];
+            const float* Sq = S + q * kLd;
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Sq[jj * K + a + 1] - Sq[jj * K + a], Sq[jj * K + a]);
         }
     }
-    __syncthreads();
 
-    // interpolation: thread (q, a) produces the D outputs of x-offset a for query q
-    for (int idx = tid; idx < kQ * D; idx += kThreads) {
+    // y-interpolation and the (a, b)-major output planes
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int idx = tid + i * kLookThreads;
+        if (idx >= kQ * D) break;
         const int q = idx % kQ, a = idx / kQ;
         const int y = qy0 + q / kBX, x = qx0 + q % kBX;
         if (y >= g.H || x >= g.W) continue;
-        int xs, ys;
-        float fx, fy;
-        origin(q, xs, ys, fx, fy);
-        float hx[K];
-#pragma unroll
-        for (int jj = 0; jj < K; ++jj) {
-            const int ty = ys + jj;
-            float v[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int tx = xs + a + u;
-                float e = 0.f;
-                if (ty >= 0 && ty < lh && tx >= 0 && tx < lw)
-                    e = dense ? S[q * kMaxT + (ty - by0) * tw + (tx - bx0)] : S[q * KK + jj * K + a + u];
-                v[u] = e;
-            }
-            hx[jj] = fmaf(fx, v[1] - v[0], v[0]);
-        }
+        const float fy = sfy[q];
         float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
-        for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[bb + 1] - hx[bb], hx[bb]);
+        for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
     }
 }
 
@@ -251,6 +369,12 @@ int check_otf(int batch, int channels, int height, int width, int levels, int co
     return RMD_OK;
 }
 
+template <typename T>
+void launch_segments(const LevelSrc& src, const OtfGeom& g, float scale, T* seg, hipStream_t st) {
+    const long long n = (long long)g.B * g.TS * (g.Cp / Seg<T>::LSC) * 64;
+    otf_segments_kernel<T><<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, st>>>(src, g, scale, seg);
+}
+
 }  // namespace
 }  // namespace rmd
 
@@ -261,7 +385,7 @@ extern "C" size_t rmd_corr_otf_workspace_bytes(int batch, int channels, int heig
     if (check_otf(batch, channels, height, width, levels, compute)) return 0;
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
     const size_t es = compute == RMD_F32 ? 4 : 2;
-    return (size_t)batch * ((size_t)height * width + g.T) * g.Cp * es;
+    return otf_scratch_offset(g, es) + otf_scratch_elems(g) * 4;
 }
 
 extern "C" int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int batch, int channels, int height,
@@ -271,19 +395,28 @@ extern "C" int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int 
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
-    const OtfGeom g1 = make_otf_geom(batch, channels, height, width, 1);
-    const long long nq = (long long)batch * g1.T * (g.Cp / 8), nt = (long long)batch * g.T * (g.Cp / 8);
-    const unsigned gq = (unsigned)((nq + kThreads - 1) / kThreads), gt = (unsigned)((nt + kThreads - 1) / kThreads);
+    const OtfGeom g1 = make_otf_geom(batch, channels, height, width, 1);   // query segments: TS = QS
+    const size_t es = compute == RMD_F32 ? 4 : 2;
+    LevelSrc lq{}, lt{};
+    lq.p[0] = fmap1;
+    lt.p[0] = fmap2;
+    float* scratch = reinterpret_cast<float*>(static_cast<char*>(workspace) + otf_scratch_offset(g, es));
+    for (int l = 1; l < levels; ++l) {
+        const long long n = (long long)batch * channels * g.lh[l] * g.lw[l];
+        otf_pool2_kernel<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, st>>>(
+            lt.p[l - 1], batch * channels, g.lh[l - 1], g.lw[l - 1], scratch);
+        lt.p[l] = scratch;
+        scratch += n;
+    }
+    const size_t qn = otf_query_elems(g);
     if (compute == RMD_BF16) {
         __bf16* q = reinterpret_cast<__bf16*>(workspace);
-        __bf16* t = q + (size_t)batch * height * width * g.Cp;
-        otf_rows_kernel<__bf16><<<gq, kThreads, 0, st>>>(fmap1, g1, scale, q);
-        otf_rows_kernel<__bf16><<<gt, kThreads, 0, st>>>(fmap2, g, 1.0f, t);
+        launch_segments<__bf16>(lq, g1, scale, q, st);
+        launch_segments<__bf16>(lt, g, 1.0f, q + qn, st);
     } else {
         float* q = reinterpret_cast<float*>(workspace);
-        float* t = q + (size_t)batch * height * width * g.Cp;
-        otf_rows_kernel<float><<<gq, kThreads, 0, st>>>(fmap1, g1, scale, q);
-        otf_rows_kernel<float><<<gt, kThreads, 0, st>>>(fmap2, g, 1.0f, t);
+        launch_segments<float>(lq, g1, scale, q, st);
+        launch_segments<float>(lt, g, 1.0f, q + qn, st);
     }
     return check_launch("rmd_corr_otf_prepare");
 }
@@ -297,27 +430,36 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: radius %d not in 1..8", radius);
     hipStream_t st = as_stream(stream);
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
-    dim3 grid(((width + kBX - 1) / kBX) * ((height + kBY - 1) / kBY), levels, batch);
-    const size_t lds = sizeof(float) * kQ * kMaxT;
-    const size_t qn = (size_t)batch * height * width * g.Cp;
-#define RMD_OTF(T, RR)                                                                                         \
+    const long long nblk = (long long)((width + kBX - 1) / kBX) * ((height + kBY - 1) / kBY) * levels * batch;
+    RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");
+    const size_t lds = sizeof(float) * kQ * kLd;
+    const size_t qn = otf_query_elems(g);
+#define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \
-        auto k = otf_lookup_kernel<T, RR>;                                                                     \
+        auto k = otf_lookup_kernel<T, RR, CC>;                                                                 \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
-        k<<<grid, kThreads, lds, st>>>(q, q + qn, g, coords, zero_level_mask, out);                            \
+        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn, g, coords, zero_level_mask, out);              \
     } while (0)
+#define RMD_OTF_C(T, RR)                                 \
+    switch (g.Cp) {                                      \
+        case 32: RMD_OTF(T, RR, 32); break;              \
+        case 64: RMD_OTF(T, RR, 64); break;              \
+        case 128: RMD_OTF(T, RR, 128); break;            \
+        case 256: RMD_OTF(T, RR, 256); break;            \
+        default: RMD_OTF(T, RR, 0); break;               \
+    }
 #define RMD_OTF_R(T)                                     \
     switch (radius) {                                    \
-        case 1: RMD_OTF(T, 1); break;                    \
-        case 2: RMD_OTF(T, 2); break;                    \
-        case 3: RMD_OTF(T, 3); break;                    \
-        case 4: RMD_OTF(T, 4); break;                    \
-        case 5: RMD_OTF(T, 5); break;                    \
-        case 6: RMD_OTF(T, 6); break;                    \
-        case 7: RMD_OTF(T, 7); break;                    \
-        default: RMD_OTF(T, 8); break;                   \
+        case 1: RMD_OTF_C(T, 1); break;                  \
+        case 2: RMD_OTF_C(T, 2); break;                  \
+        case 3: RMD_OTF_C(T, 3); break;                  \
+        case 4: RMD_OTF_C(T, 4); break;                  \
+        case 5: RMD_OTF_C(T, 5); break;                  \
+        case 6: RMD_OTF_C(T, 6); break;                  \
+        case 7: RMD_OTF_C(T, 7); break;                  \
+        default: RMD_OTF_C(T, 8); break;                 \
     }
     if (compute == RMD_BF16) {
         RMD_OTF_R(__bf16)
@@ -325,6 +467,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         RMD_OTF_R(float)
     }
 #undef RMD_OTF_R
+#undef RMD_OTF_C
 #undef RMD_OTF
     return check_launch("rmd_corr_otf_lookup");
 }

@@ -49,7 +49,7 @@ CASES = [
     (2, 32, 24, 40, 4, 4, 2.0, ()),
     (1, 40, 17, 23, 3, 3, 3.0, (4,)),          # C not a multiple of 32, ragged map, level 1 masked
     (2, 64, 12, 20, 4, 2, 1.0, ()),            # level 3 is 1x2 -> NaN
-    (1, 16, 30, 50, 2, 7, 25.0, ()),           # huge spread: union boxes overflow -> fallback
+    (1, 16, 30, 50, 2, 7, 25.0, ()),           # huge spread: union boxes span many bands
     (1, 256, 46, 62, 4, 4, 4.0, (3, 6)),       # cfg1 feature shape, levels 0 and 3 masked
     (1, 8, 9, 70, 1, 1, 0.5, ()),              # one level, r=1, wide map
 ]
@@ -71,6 +71,20 @@ def test_otf_matches_oracle(case, precision):
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     fin = ~np.isnan(ref)
     assert rel_max_err(got[fin], ref[fin]) < TOL[precision]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_otf_wide_box_per_query_path(precision):
+    """Flow scattered over a 600-pixel-wide map: union boxes wider than kMaxT take the per-query path."""
+    import rmd
+    rng = np.random.default_rng(9)
+    b, c, h, w = 1, 24, 4, 600
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    co = np.stack([rng.uniform(-5, w + 5, (b, h, w)), rng.uniform(-2, h + 2, (b, h, w))], 1).astype(np.float32)
+    ref = oracle.corr_lookup_fs(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64), 2, 3)
+    got = rmd.raft_fs.CorrBlock(_t(f1), _t(f2), 2, 3, precision=precision, method="otf")(_t(co)).cpu().numpy()
+    assert rel_max_err(got, ref) < TOL[precision]
 
 
 def test_otf_dot_scale_one_level():
