@@ -13,7 +13,7 @@
 // so operand loads are whole 128-B lines (the row-per-lane gather of a pixel-major layout touches 32
 // lines per instruction and halves the L1 rate).  Query rows (fmap1 * scale) use the same layout.
 //
-// Lookup: one 256-thread block per (16 x 2 query block, level, batch).  The 32 queries' (2r+2)^2
+// Lookup: one 256-thread block per (16 x 2 query block, batch), looping over the levels.  The 32 queries' (2r+2)^2
 // integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
 // processed in bands of whole rows of at most kMaxT targets: S = band targets x queries, one 16x16
 // MFMA tile per (target segment, query segment), into LDS.  Each (query, x-offset) thread keeps its
@@ -167,12 +167,14 @@ __device__ __forceinline__ float seg_elem(const T* segbase, int i, int c) {
     return (float)segbase[(c / S::LSC) * 64 * S::LE + (S::lane_g(c) * 16 + i) * S::LE + S::elem(c)];
 }
 
-// 1-D grid over (batch, level, query block), XCD-aware: adjacent query blocks, whose target boxes
-// overlap, run on the same XCD and share its L2.  CPT = compiled Cp (0: runtime multiple of 128).
+// 1-D grid over (batch, query block), XCD-aware: adjacent query blocks, whose target boxes overlap,
+// run on the same XCD and share its L2.  One block runs every level of its 32 queries, so the query
+// staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
+// CPT = compiled Cp (0: runtime multiple of 128).
 template <typename T, int R, int CPT>
 __global__ void __launch_bounds__(kLookThreads)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
-                  const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
+                  const float* __restrict__ coords, unsigned zmask, float* __restrict__ out, int ablate) {
     using SG = Seg<T>;
     using frag = typename SG::frag;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K;
@@ -184,115 +186,182 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
     const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
-    const int qb = lid % nqb, L = (lid / nqb) % g.L, b = lid / (nqb * g.L);
+    const int qb = lid % nqb, b = lid / nqb;
     const int qx0 = (qb % nbx) * kBX, qy0 = (qb / nbx) * kBY;
     const int N = g.H * g.W;
-    const int lh = g.lh[L], lw = g.lw[L];
-    const int tid = threadIdx.x;
-    float* ob = out + ((size_t)b * g.L + L) * D * D * (size_t)N;
-
-    // masked / degenerate level: constant output (raft_fs.py:77-78; 1-pixel levels divide by zero)
-    const bool masked = (zmask >> L) & 1u;
-    if (masked || lh < 2 || lw < 2) {
-        const float v = masked ? 0.f : __builtin_nanf("");
-        for (int idx = tid; idx < kQ * D * D; idx += kLookThreads) {
-            const int q = idx % kQ, c = idx / kQ;
-            const int y = qy0 + q / kBX, x = qx0 + q % kBX;
-            if (y < g.H && x < g.W) ob[(size_t)c * N + y * g.W + x] = v;
-        }
-        return;
-    }
-
-    if (tid == 0) {
-        box[0] = 1 << 30;
-        box[1] = -(1 << 30);
-        box[2] = 1 << 30;
-        box[3] = -(1 << 30);
-    }
-    __syncthreads();
-    if (tid < kQ) {
-        // query's window origin at level L (coords clamped as rmd_corr_lookup does)
-        const int y = min(qy0 + tid / kBX, g.H - 1), x = min(qx0 + tid % kBX, g.W - 1);
-        const float inv = 1.0f / (float)(1 << L);
-        float cx = coords[((size_t)b * 2 + 0) * N + y * g.W + x] * inv;
-        float cy = coords[((size_t)b * 2 + 1) * N + y * g.W + x] * inv;
-        cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
-        cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
-        const float fx0 = floorf(cx), fy0 = floorf(cy);
-        const int xs = (int)fx0 - R, ys = (int)fy0 - R;
-        sxs[tid] = xs;
-        sys[tid] = ys;
-        sfx[tid] = cx - fx0;
-        sfy[tid] = cy - fy0;
-        atomicMin(&box[0], xs);
-        atomicMax(&box[1], xs + K - 1);
-        atomicMin(&box[2], ys);
-        atomicMax(&box[3], ys + K - 1);
-    }
-    __syncthreads();
-    const int bx0 = max(box[0], 0), bx1 = min(box[1], lw - 1);
-    const int by0 = max(box[2], 0), by1 = min(box[3], lh - 1);
-    const int th = max(by1 - by0 + 1, 0);
-    const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0, sw = nseg * 16;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cp = CPT > 0 ? CPT : g.Cp;
     const int nls = cp / SG::LSC;
     const size_t segsz = (size_t)16 * cp;
     const T* qsb = qseg + ((size_t)b * g.QS + (size_t)qy0 * g.qnsx + (qx0 >> 4)) * segsz;
     const T* qsb1 = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + 1, g.H - 1) * g.qnsx + (qx0 >> 4)) * segsz;
-    const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
 
+    // the block's two query segments (CPT > 0): one coalesced copy into LDS, overlapping the coords
+    // load; each wave then keeps its register fragments for every level and target segment
+    constexpr int NLS = CPT > 0 ? CPT / SG::LSC : 1;
+    constexpr int QV = CPT > 0 ? 16 * CPT * (int)sizeof(T) / 16 : 0;     // 16-B vectors per segment
+    static_assert(2 * QV * 16 <= kQ * kLd * 4, "two query segments must fit the S buffer");
+    if constexpr (CPT > 0) {
+        const uint4* s0 = reinterpret_cast<const uint4*>(qsb);
+        const uint4* s1 = reinterpret_cast<const uint4*>(qsb1);
+        uint4* dst = reinterpret_cast<uint4*>(S);
+        for (int v = tid; v < QV; v += kLookThreads) {
+            dst[v] = s0[v];
+            dst[QV + v] = s1[v];
+        }
+    }
+    float cx0 = 0.f, cy0 = 0.f;
+    if (tid < kQ) {
+        const int y = min(qy0 + tid / kBX, g.H - 1), x = min(qx0 + tid % kBX, g.W - 1);
+        cx0 = coords[((size_t)b * 2 + 0) * N + y * g.W + x];
+        cy0 = coords[((size_t)b * 2 + 1) * N + y * g.W + x];
+    }
+    __syncthreads();
+    frag q0[NLS], q1[NLS];
+    if constexpr (CPT > 0) {
+        const frag* qs = reinterpret_cast<const frag*>(S);
+#pragma unroll
+        for (int ls = 0; ls < NLS; ++ls) {
+            q0[ls] = qs[ls * 64 + lane];
+            q1[ls] = qs[(NLS + ls) * 64 + lane];
+        }
+    }
     // thread items (q, a): query q, window x-offset a; hx[i][jj] = row jj of the window, x-interpolated
     constexpr int ITEMS = (kQ * D + kLookThreads - 1) / kLookThreads;
-    float hx[ITEMS][K];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i)
-#pragma unroll
-        for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
 
-    if (sw <= kMaxT) {
-        const int lane = tid & 63, w = tid >> 6;
-        const int bh = sw > 0 ? kMaxT / sw : 1;
-        // the block's two query segments, held in registers for every target segment (CPT > 0)
-        constexpr int NLS = CPT > 0 ? CPT / SG::LSC : 1;
-        frag q0[NLS], q1[NLS];
-        if constexpr (CPT > 0) {
-#pragma unroll
-            for (int ls = 0; ls < NLS; ++ls) {
-                q0[ls] = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
-                q1[ls] = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
+    for (int L = 0; L < g.L; ++L) {
+        const int lh = g.lh[L], lw = g.lw[L];
+        float* ob = out + ((size_t)b * g.L + L) * D * D * (size_t)N;
+        // masked / degenerate level: constant output (raft_fs.py:77-78; 1-pixel levels divide by zero)
+        const bool masked = (zmask >> L) & 1u;
+        if (masked || lh < 2 || lw < 2) {
+            const float v = masked ? 0.f : __builtin_nanf("");
+            for (int idx = tid; idx < kQ * D * D; idx += kLookThreads) {
+                const int q = idx % kQ, c = idx / kQ;
+                const int y = qy0 + q / kBX, x = qx0 + q % kBX;
+                if (y < g.H && x < g.W) ob[(size_t)c * N + y * g.W + x] = v;
             }
+            continue;
         }
-        for (int ry0 = by0; ry0 < by0 + th; ry0 += bh) {
-            const int nrow = min(bh, by0 + th - ry0), ntask = nrow * nseg;
-            for (int task = w; task < ntask; task += kWaves) {
-                const int trow = ry0 + task / nseg, ts = task % nseg;
-                const T* tsb = tlev + ((size_t)trow * g.nsx[L] + sa + ts) * segsz + (size_t)lane * SG::LE;
-                f32x4 a0 = {}, a1 = {};
+        if (tid == 0) {
+            box[0] = 1 << 30;
+            box[1] = -(1 << 30);
+            box[2] = 1 << 30;
+            box[3] = -(1 << 30);
+        }
+        __syncthreads();                               // also: S / box of the previous level are free
+        if (tid < kQ) {
+            // query's window origin at level L (coords clamped as rmd_corr_lookup does)
+            const float inv = 1.0f / (float)(1 << L);
+            const float cx = fminf(fmaxf(cx0 * inv, -1.0e6f), 1.0e6f);
+            const float cy = fminf(fmaxf(cy0 * inv, -1.0e6f), 1.0e6f);
+            const float fx0 = floorf(cx), fy0 = floorf(cy);
+            const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+            sxs[tid] = xs;
+            sys[tid] = ys;
+            sfx[tid] = cx - fx0;
+            sfy[tid] = cy - fy0;
+            atomicMin(&box[0], xs);
+            atomicMax(&box[1], xs + K - 1);
+            atomicMin(&box[2], ys);
+            atomicMax(&box[3], ys + K - 1);
+        }
+        __syncthreads();
+        const int bx0 = max(box[0], 0), bx1 = min(box[1], lw - 1);
+        const int by0 = max(box[2], 0), by1 = min(box[3], lh - 1);
+        const int th = max(by1 - by0 + 1, 0);
+        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0, sw = nseg * 16;
+        const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
+
+        float hx[ITEMS][K];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
+
+        if (sw <= kMaxT) {
+            const int bh = sw > 0 ? kMaxT / sw : 1;
+            for (int ry0 = by0; ry0 < by0 + th; ry0 += bh) {
+                const int nrow = min(bh, by0 + th - ry0), ntask = nrow * nseg;
+                // C[target 4*(lane>>4)+e][query lane&15] -> S[query][band target]
+                auto store = [&](const f32x4& a0, const f32x4& a1, int task) {
+                    const int col = (task / nseg) * sw + (task % nseg) * 16 + 4 * (lane >> 4), j = lane & 15;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        S[j * kLd + col + e] = a0[e];
+                        S[(16 + j) * kLd + col + e] = a1[e];
+                    }
+                };
+                auto tptr = [&](int task) {
+                    return tlev + ((size_t)(ry0 + task / nseg) * g.nsx[L] + sa + task % nseg) * segsz +
+                           (size_t)lane * SG::LE;
+                };
                 if constexpr (CPT > 0) {
-                    frag t[NLS];
+                    for (int task = w; task < ntask; task += kWaves) {
+                        if (ablate & 2) break;
+                        const T* tsb = tptr(task);
+                        frag t[NLS];
 #pragma unroll
-                    for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                        for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                        f32x4 a0 = {}, a1 = {};
 #pragma unroll
-                    for (int ls = 0; ls < NLS; ++ls) {
-                        SG::mma(a0, t[ls], q0[ls]);
-                        SG::mma(a1, t[ls], q1[ls]);
+                        for (int ls = 0; ls < NLS; ++ls) {
+                            SG::mma(a0, t[ls], q0[ls]);
+                            SG::mma(a1, t[ls], q1[ls]);
+                        }
+                        store(a0, a1, task);
                     }
                 } else {
-                    for (int ls = 0; ls < nls; ++ls) {
-                        const frag t = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-                        const frag u0 = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
-                        const frag u1 = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
-                        SG::mma(a0, t, u0);
-                        SG::mma(a1, t, u1);
+                    for (int task = w; task < ntask; task += kWaves) {
+                        const T* tsb = tptr(task);
+                        f32x4 a0 = {}, a1 = {};
+                        for (int ls = 0; ls < nls; ++ls) {
+                            const frag t = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                            const frag u0 = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
+                            const frag u1 = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
+                            SG::mma(a0, t, u0);
+                            SG::mma(a1, t, u1);
+                        }
+                        store(a0, a1, task);
                     }
                 }
-                // C[target 4*(lane>>4)+e][query lane&15] -> S[query][band target]
-                const int col = (trow - ry0) * sw + ts * 16 + 4 * (lane >> 4), j = lane & 15;
+                __syncthreads();
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    S[j * kLd + col + e] = a0[e];
-                    S[(16 + j) * kLd + col + e] = a1[e];
+                for (int i = 0; i < ITEMS; ++i) {
+                    const int idx = tid + i * kLookThreads;
+                    if (idx >= kQ * D) break;
+                    const int q = idx % kQ, a = idx / kQ;
+                    const int xs = sxs[q], ys = sys[q];
+                    const float fx = sfx[q];
+                    const float* Sq = S + q * kLd;
+#pragma unroll
+                    for (int jj = 0; jj < K; ++jj) {
+                        const int ty = ys + jj;
+                        if (ty >= ry0 && ty < ry0 + nrow) {
+                            float v[2];
+#pragma unroll
+                            for (int u = 0; u < 2; ++u) {
+                                const int tx = xs + a + u;
+                                v[u] = (tx >= 0 && tx < lw) ? Sq[(ty - ry0) * sw + (tx - sa * 16)] : 0.f;
+                            }
+                            hx[i][jj] = fmaf(fx, v[1] - v[0], v[0]);
+                        }
+                    }
                 }
+                __syncthreads();
+            }
+        } else {
+            // box wider than kMaxT: each query's own (2r+2)^2 patch, one dot product per thread
+            for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
+                const int q = idx / KK, r = idx - q * KK;
+                const int ty = sys[q] + r / K, tx = sxs[q] + r % K;
+                float acc = 0.f;
+                if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
+                    const T* qs = q < kBX ? qsb : qsb1;
+                    const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
+                    for (int c = 0; c < g.C; ++c) acc = fmaf(seg_elem(qs, q % kBX, c), seg_elem(ts, tx & 15, c), acc);
+                }
+                S[q * kLd + r] = acc;
             }
             __syncthreads();
 #pragma unroll
@@ -300,63 +369,30 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 const int idx = tid + i * kLookThreads;
                 if (idx >= kQ * D) break;
                 const int q = idx % kQ, a = idx / kQ;
-                const int xs = sxs[q], ys = sys[q];
                 const float fx = sfx[q];
                 const float* Sq = S + q * kLd;
 #pragma unroll
-                for (int jj = 0; jj < K; ++jj) {
-                    const int ty = ys + jj;
-                    if (ty >= ry0 && ty < ry0 + nrow) {
-                        float v[2];
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            const int tx = xs + a + u;
-                            v[u] = (tx >= 0 && tx < lw) ? Sq[(ty - ry0) * sw + (tx - sa * 16)] : 0.f;
-                        }
-                        hx[i][jj] = fmaf(fx, v[1] - v[0], v[0]);
-                    }
-                }
+                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Sq[jj * K + a + 1] - Sq[jj * K + a], Sq[jj * K + a]);
             }
-            __syncthreads();
         }
-    } else {
-        // box wider than kMaxT: each query's own (2r+2)^2 patch, one dot product per thread
-        for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
-            const int q = idx / KK, r = idx - q * KK;
-            const int ty = sys[q] + r / K, tx = sxs[q] + r % K;
-            float acc = 0.f;
-            if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
-                const T* qs = q < kBX ? qsb : qsb1;
-                const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
-                for (int c = 0; c < g.C; ++c) acc = fmaf(seg_elem(qs, q % kBX, c), seg_elem(ts, tx & 15, c), acc);
-            }
-            S[q * kLd + r] = acc;
-        }
-        __syncthreads();
+
+        // y-interpolation and the (a, b)-major output planes
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
             const int idx = tid + i * kLookThreads;
             if (idx >= kQ * D) break;
             const int q = idx % kQ, a = idx / kQ;
-            const float fx = sfx[q];
-            const float* Sq = S + q * kLd;
+            const int y = qy0 + q / kBX, x = qx0 + q % kBX;
+            if (y >= g.H || x >= g.W) continue;
+            const float fy = sfy[q];
+            if (ablate & 1) {
+                if (hx[i][0] == 123.f) ob[0] = fy;       // keep the sums live
+                continue;
+            }
+            float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
-            for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Sq[jj * K + a + 1] - Sq[jj * K + a], Sq[jj * K + a]);
+            for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
         }
-    }
-
-    // y-interpolation and the (a, b)-major output planes
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int idx = tid + i * kLookThreads;
-        if (idx >= kQ * D) break;
-        const int q = idx % kQ, a = idx / kQ;
-        const int y = qy0 + q / kBX, x = qx0 + q % kBX;
-        if (y >= g.H || x >= g.W) continue;
-        const float fy = sfy[q];
-        float* o = ob + (size_t)(a * D) * N + y * g.W + x;
-#pragma unroll
-        for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
     }
 }
 
@@ -430,20 +466,27 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: radius %d not in 1..8", radius);
     hipStream_t st = as_stream(stream);
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
-    const long long nblk = (long long)((width + kBX - 1) / kBX) * ((height + kBY - 1) / kBY) * levels * batch;
+    const long long nblk = (long long)((width + kBX - 1) / kBX) * ((height + kBY - 1) / kBY) * batch;
     RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");
     const size_t lds = sizeof(float) * kQ * kLd;
     const size_t qn = otf_query_elems(g);
+    // compiled channel counts keep the query segments in registers; f32 operands of >= 128 channels
+    // would not fit and take the runtime loop (RMD_OTF_RUNTIME=1 forces it for A/B runs)
+    // RMD_OTF_ABLATE (diagnostics only, results invalid): bits 1 = skip output stores, 2 = skip the MFMA
+    // phase
+    static const int ablate = getenv("RMD_OTF_ABLATE") ? atoi(getenv("RMD_OTF_ABLATE")) : 0;
+    static const bool force_rt = getenv("RMD_OTF_RUNTIME") && atoi(getenv("RMD_OTF_RUNTIME")) != 0;
+    const int cpt = force_rt || (compute == RMD_F32 && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
 #define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \
         auto k = otf_lookup_kernel<T, RR, CC>;                                                                 \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
-        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn, g, coords, zero_level_mask, out);              \
+        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn, g, coords, zero_level_mask, out, ablate);              \
     } while (0)
 #define RMD_OTF_C(T, RR)                                 \
-    switch (g.Cp) {                                      \
+    switch (cpt) {                                       \
         case 32: RMD_OTF(T, RR, 32); break;              \
         case 64: RMD_OTF(T, RR, 64); break;              \
         case 128: RMD_OTF(T, RR, 128); break;            \
