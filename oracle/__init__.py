@@ -1,7 +1,6 @@
 """CPU restatement of qzed/raft-meets-dicl's cost-volume hot path — TEST INFRASTRUCTURE ONLY.
 
-This package is the parity oracle.  It restates the reference algorithm directly (numpy; plain C
-for the timed CPU-baseline lookup in ``oracle/c/``) and is pinned against golden vectors produced
+This package is the parity oracle.  It restates the reference algorithm directly (numpy) and is pinned against golden vectors produced
 by running the reference itself (``tests/golden/gen_golden.py``; checked by
 ``tests/test_oracle_golden.py``).
 
@@ -13,7 +12,9 @@ product path (``raft-meets-dicl_amd/``) never imports it and has no CPU fallback
 from .corr import (corr_volume, corr_pyramid, corr_lookup, corr_lookup_fs, corr_lookup_backward,
                    pyramid_level_shapes)
 from .dicl import dicl_stack, dicl_stack_backward, dicl_stack_int, dicl_stack_int_backward, dap, dap_backward
+from .heads import up8, up8_backward, softargmax, softargmax_backward
 
 __all__ = ["corr_volume", "corr_pyramid", "corr_lookup", "corr_lookup_fs", "corr_lookup_backward",
            "pyramid_level_shapes", "dicl_stack", "dicl_stack_backward", "dicl_stack_int",
-           "dicl_stack_int_backward", "dap", "dap_backward"]
+           "dicl_stack_int_backward", "dap", "dap_backward", "up8", "up8_backward", "softargmax",
+           "softargmax_backward"]
