@@ -210,6 +210,44 @@ int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* fmap2, int 
 int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose, float* out,
             void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Per-iteration flow heads on either side of the lookup.
+ */
+
+/*
+ * Convex 8x upsampling.  Replaces the tail of Up8Network.forward (src/models/impls/raft.py:319-331)
+ * after its two convolutions: mask (B, 576, h, w) logits with channel = k*64 + i*8 + j (neighbour
+ * k = 3*ky + kx, sub-pixel (i, j)), flow (B, 2, h, w) ->
+ *   out[b, c, 8y+i, 8x+j] = sum_k softmax_k(mask[b, k*64+i*8+j, y, x] / temperature) * 8*flow[b, c, y+ky-1, x+kx-1]
+ * (zero outside the map; F.unfold(8*flow, 3, padding=1)).  out (B, 2, 8h, 8w) float32.
+ */
+int rmd_up8(const float* mask, const float* flow, int batch, int height, int width, float temperature,
+            float* out, void* stream);
+
+/* Bytes of device workspace rmd_up8_backward needs (per-pixel neighbour sums, 72 B/pixel). */
+size_t rmd_up8_workspace_bytes(int batch, int height, int width);
+
+/* Gradients of rmd_up8 w.r.t. mask (B, 576, h, w) and flow (B, 2, h, w); deterministic (no atomics). */
+int rmd_up8_backward(const float* mask, const float* flow, const float* grad_out, int batch, int height, int width,
+                     float temperature, float* grad_mask, float* grad_flow, void* workspace, void* stream);
+
+/*
+ * Soft-argmax flow regression.  Replaces raft.SoftArgMaxFlowRegression.forward (raft.py:112-135;
+ * levels = L, level l scaled by 2^l) and the single-level SoftArgMaxFlowRegression of
+ * corr/dicl.py:64-85, corr/dot.py:69-90, dicl_1x1.py:89-110, dicl_emb.py:107-134 (levels = 1):
+ *   p_k = softmax_k(cost[b, l*(2r+1)^2 + k, :] / temperature),  k = a*(2r+1) + bb,
+ *   flows[l, b, 0] = 2^l * sum_k p_k (a - r),  flows[l, b, 1] = 2^l * sum_k p_k (bb - r).
+ * cost (B, cost_channels, pixels) float32 with cost_channels >= L*(2r+1)^2 (extra trailing channels
+ * are ignored: dicl_emb regresses on the first (2r+1)^2 of its embedding); flows (L, B, 2, pixels).
+ * radius 1..4.  The *WithDap variants run rmd_dap on each level first (raft.py:139-181).
+ */
+int rmd_softargmax(const float* cost, int batch, int cost_channels, int pixels, int levels, int radius,
+                   float temperature, float* flows, void* stream);
+
+/* d cost for channels [0, L*(2r+1)^2) of each batch row (others untouched) from grad_flows (L, B, 2, pixels). */
+int rmd_softargmax_backward(const float* cost, const float* grad_flows, int batch, int cost_channels, int pixels,
+                            int levels, int radius, float temperature, float* grad_cost, void* stream);
+
 /* Message for the last failing call on this thread ("" if none). */
 const char* rmd_last_error(void);
 

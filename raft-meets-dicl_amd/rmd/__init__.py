@@ -9,9 +9,10 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.raft_dicl_ml.CorrelationModule    <- src/models/impls/raft_dicl_ml.py:235-343
   rmd.blocks.dicl                       <- src/models/common/blocks/dicl.py:93-150
   rmd.dicl.compute_cost                 <- src/models/impls/dicl.py:212-241
+  rmd.raft.Up8Network / SoftArgMax*     <- src/models/impls/raft.py:98-190,299-331 (rmd.heads)
 """
 
-from . import blocks, corr, dicl, ops, raft, raft_dicl_ml, raft_fs  # noqa: F401
+from . import blocks, corr, dicl, heads, ops, raft, raft_dicl_ml, raft_fs  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

@@ -61,6 +61,11 @@ _SIGS = {
     "rmd_dicl_stack_int": (_I, [_P, _P] + [_I] * 6 + [_P, _P, _P]),
     "rmd_dicl_stack_int_backward": (_I, [_P, _P] + [_I] * 6 + [_P, _P, _P, _P]),
     "rmd_dap": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "rmd_up8": (_I, [_P, _P, _I, _I, _I, ctypes.c_float, _P, _P]),
+    "rmd_up8_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I]),
+    "rmd_up8_backward": (_I, [_P, _P, _P, _I, _I, _I, ctypes.c_float, _P, _P, _P, _P]),
+    "rmd_softargmax": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
+    "rmd_softargmax_backward": (_I, [_P, _P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_last_error": (ctypes.c_char_p, []),
     "rmd_version": (ctypes.c_char_p, []),
 }

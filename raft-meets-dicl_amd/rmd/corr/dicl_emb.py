@@ -49,3 +49,8 @@ class CorrelationModule(nn.Module):
         score = F.softmax(score.view(batch, (2 * r + 1) ** 2, h, w), dim=1).view(batch, 2 * r + 1, 2 * r + 1, 1, h, w)
         emb = (score * emb).sum(dim=(1, 2))
         return torch.cat((cost.view(batch, -1, h, w), emb), dim=1)
+
+
+# single-level soft-argmax regressions of this module (reference classes of the same names)
+from ..heads import CorrSoftArgMaxFlowRegression as SoftArgMaxFlowRegression  # noqa: E402,F401
+from ..heads import CorrSoftArgMaxFlowRegressionWithDap as SoftArgMaxFlowRegressionWithDap  # noqa: E402,F401

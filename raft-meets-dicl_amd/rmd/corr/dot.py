@@ -40,3 +40,8 @@ class CorrelationModule(nn.Module):
         if dap:
             corr = self.dap(corr)
         return corr.reshape(batch, -1, h, w)
+
+
+# single-level soft-argmax regressions of this module (reference classes of the same names)
+from ..heads import CorrSoftArgMaxFlowRegression as SoftArgMaxFlowRegression  # noqa: E402,F401
+from ..heads import CorrSoftArgMaxFlowRegressionWithDap as SoftArgMaxFlowRegressionWithDap  # noqa: E402,F401

@@ -405,3 +405,85 @@ class _Dap(torch.autograd.Function):
 def dap(x, weight):
     """x (B, D, ...) -> W x over the displacement dim; weight (D, D[, 1, 1])."""
     return _Dap.apply(x, weight)
+
+
+# ---- per-iteration flow heads (rmd_up8, rmd_softargmax) -----------------------------------------
+
+class _Up8(torch.autograd.Function):
+    """Convex 8x upsampling after Up8Network's convolutions — raft.py:319-331."""
+
+    @staticmethod
+    def forward(ctx, mask, flow, temperature):
+        _require_gpu(mask, flow)
+        b, c, h, w = flow.shape
+        if c != 2 or tuple(mask.shape) != (b, 576, h, w):
+            raise ValueError(f"up8: need flow (B,2,h,w) and mask (B,576,h,w), got {tuple(flow.shape)}, "
+                             f"{tuple(mask.shape)}")
+        mc = mask.detach().float().contiguous()
+        fc = flow.detach().float().contiguous()
+        out = torch.empty((b, 2, 8 * h, 8 * w), dtype=torch.float32, device=fc.device)
+        with torch.cuda.device(fc.device):
+            _lib.check(_lib.lib().rmd_up8(_ptr(mc), _ptr(fc), b, h, w, float(temperature), _ptr(out), _stream(fc)),
+                       "rmd_up8")
+        ctx.save_for_backward(mc, fc)
+        ctx.temperature = float(temperature)
+        ctx.dtypes = (mask.dtype, flow.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        mc, fc = ctx.saved_tensors
+        b, _, h, w = fc.shape
+        g = grad.float().contiguous()
+        lib = _lib.lib()
+        ws = torch.empty(lib.rmd_up8_workspace_bytes(b, h, w), dtype=torch.uint8, device=g.device)
+        gm = torch.empty_like(mc)
+        gf = torch.empty_like(fc)
+        with torch.cuda.device(g.device):
+            _lib.check(lib.rmd_up8_backward(_ptr(mc), _ptr(fc), _ptr(g), b, h, w, ctx.temperature, _ptr(gm), _ptr(gf),
+                                            _ptr(ws), _stream(g)), "rmd_up8_backward")
+        return gm.to(ctx.dtypes[0]), gf.to(ctx.dtypes[1]), None
+
+
+def up8(mask, flow, temperature=4.0):
+    """mask (B, 576, h, w) logits, flow (B, 2, h, w) -> convex-upsampled flow (B, 2, 8h, 8w)."""
+    return _Up8.apply(mask, flow, temperature)
+
+
+class _SoftArgMax(torch.autograd.Function):
+    """Soft-argmax over each level's (2r+1)^2 costs — raft.py:112-135, corr/dot.py:83-90."""
+
+    @staticmethod
+    def forward(ctx, cost, levels, radius, temperature):
+        _require_gpu(cost)
+        b, ctot = cost.shape[:2]
+        n = cost[0, 0].numel()
+        dd = (2 * radius + 1) ** 2
+        if ctot < levels * dd:
+            raise ValueError(f"softargmax: {ctot} channels < {levels} levels x {dd} displacements")
+        cc = cost.detach().float().contiguous()
+        flows = torch.empty((levels, b, 2) + tuple(cost.shape[2:]), dtype=torch.float32, device=cc.device)
+        with torch.cuda.device(cc.device):
+            _lib.check(_lib.lib().rmd_softargmax(_ptr(cc), b, ctot, n, levels, radius, float(temperature), _ptr(flows),
+                                                 _stream(cc)), "rmd_softargmax")
+        ctx.save_for_backward(cc)
+        ctx.meta = (levels, radius, float(temperature), cost.dtype)
+        return flows
+
+    @staticmethod
+    def backward(ctx, gflows):
+        (cc,) = ctx.saved_tensors
+        levels, radius, temperature, dtype = ctx.meta
+        b, ctot = cc.shape[:2]
+        n = cc[0, 0].numel()
+        g = gflows.float().contiguous()
+        gc = torch.zeros_like(cc) if ctot > levels * (2 * radius + 1) ** 2 else torch.empty_like(cc)
+        with torch.cuda.device(g.device):
+            _lib.check(_lib.lib().rmd_softargmax_backward(_ptr(cc), _ptr(g), b, ctot, n, levels, radius, temperature,
+                                                          _ptr(gc), _stream(g)), "rmd_softargmax_backward")
+        return gc.to(dtype), None, None, None
+
+
+def softargmax(cost, levels, radius, temperature=1.0):
+    """cost (B, >= L*(2r+1)^2, h, w) -> list of L flows (B, 2, h, w), level l scaled by 2^l."""
+    return list(_SoftArgMax.apply(cost, levels, radius, temperature).unbind(0))

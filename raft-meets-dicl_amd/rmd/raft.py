@@ -41,3 +41,8 @@ class CorrBlock:
         if self._token is not None and torch.is_grad_enabled():
             return ops.corr_lookup_autograd(self._token, self._state, coords, self.radius, mask_costs)
         return ops.corr_lookup(self.pyramid, coords, self.radius, mask_costs)
+
+
+# per-iteration heads of raft.py (Up8Network :299-331, soft-argmax regressions :98-190)
+from .heads import (Up8Network, SoftArgMaxFlowRegression, SoftArgMaxFlowRegressionWithDap,  # noqa: E402,F401
+                    make_flow_regression)

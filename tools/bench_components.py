@@ -12,8 +12,10 @@ reports algorithmic HBM bytes per launch, GB/s and the fraction of the 8 TB/s HB
   * a4  raft_fs.CorrBlock forward at cfg2 (pyramid with scale 1 + 12 lookups), bf16
 The MatchingNet that consumes a6/a8 (MIOpen convolutions, out of scope) is timed beside them.
   * f1  on-the-fly lookup (rmd_corr_otf_*) at cfg2: prepare + per-lookup time, bf16 / fp32
-usage: python tools/bench_components.py [reps] [fs]   -> one JSON document on stdout
-      ('fs' runs only the a4 / f1 part)
+  * f2  flow heads at cfg2 (B=8, 55x128): rmd_up8 (+backward), rmd_softargmax L=4 r=4 (+backward),
+        each beside the reference's eager torch formulation on the same GPU (raft.py:112-135, 319-331)
+usage: python tools/bench_components.py [reps] [fs|heads]   -> one JSON document on stdout
+      ('fs' runs only the a4 / f1 part, 'heads' only f2)
 """
 import json
 import os
@@ -64,6 +66,11 @@ def main():
         low = torch.randn(b, 2, max(h // 8, 2), max(w // 8, 2), generator=g) * amp
         flow = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=True)
         return (torch.stack([xs, ys]).float()[None] + flow).to(dev)
+
+    if only == "heads":
+        heads(res, reps, dev, g)
+        print(json.dumps(res, indent=1))
+        return
 
     if only != "fs":
         # a6: DICL displacement stack, cfg4 1/8 level
@@ -168,6 +175,59 @@ def main():
                 lookup_GBps=(rows + out_b + cq.numel() * 4) / (t_look * 1e-3) / 1e9,
                 workspace_MB=st.ws.numel() / 1e6)
     print(json.dumps(res, indent=1))
+
+
+def heads(res, reps, dev, g):
+    """f2: per-iteration flow heads at cfg2, vs the reference's eager torch formulation (same GPU)."""
+    import torch.nn.functional as F
+    from rmd import ops
+    b, h, w = 8, 55, 128
+    n = h * w
+    mask = torch.randn(b, 576, h, w, generator=g).to(dev)
+    flow = torch.randn(b, 2, h, w, generator=g).to(dev)
+
+    def up8_eager():                       # raft.py:319-331
+        m = torch.softmax(mask.view(b, 1, 9, 8, 8, h, w) / 4.0, dim=2)
+        u = F.unfold(8 * flow, (3, 3), padding=1).view(b, 2, 9, 1, 1, h, w)
+        return torch.sum(m * u, dim=2).permute(0, 1, 4, 2, 5, 3).reshape(b, 2, h * 8, w * 8)
+
+    with torch.no_grad():
+        t = timed(lambda: ops.up8(mask, flow, 4.0), reps)
+        res["f2_up8_cfg2"] = entry(t, (b * 576 * n + b * 2 * n + b * 2 * 64 * n) * 4,
+                                   eager_torch_ms=timed(up8_eager, reps))
+    mg, fg = mask.clone().requires_grad_(True), flow.clone().requires_grad_(True)
+    go = torch.randn(b, 2, 8 * h, 8 * w, generator=g).to(dev)
+    out = ops.up8(mg, fg, 4.0)
+    t_b = timed(lambda: torch.autograd.grad(out, (mg, fg), go, retain_graph=True), reps)
+    mge, fge = mask.clone().requires_grad_(True), flow.clone().requires_grad_(True)
+    m = torch.softmax(mge.view(b, 1, 9, 8, 8, h, w) / 4.0, dim=2)
+    u = F.unfold(8 * fge, (3, 3), padding=1).view(b, 2, 9, 1, 1, h, w)
+    oute = torch.sum(m * u, dim=2).permute(0, 1, 4, 2, 5, 3).reshape(b, 2, h * 8, w * 8)
+    t_be = timed(lambda: torch.autograd.grad(oute, (mge, fge), go, retain_graph=True), reps)
+    # backward bytes: mask + grad_out read, grad_mask written, flow/q traffic (72 B/pixel x2)
+    res["f2_up8_backward_cfg2"] = entry(t_b, (2 * b * 576 * n + b * 2 * 64 * n + 2 * b * 18 * n + 4 * b * n) * 4,
+                                        eager_torch_ms=t_be)
+
+    L, r = 4, 4
+    cost = (3 * torch.randn(b, L * 81, h, w, generator=g)).to(dev)
+    d = torch.stack(torch.meshgrid(torch.linspace(-r, r, 9), torch.linspace(-r, r, 9), indexing="ij"), -1).to(dev)
+
+    def sam_eager():                       # raft.py:112-135
+        out = []
+        for lvl, c in enumerate(torch.split(cost, 81, dim=1)):
+            s = F.softmax(c.reshape(b, 81, 1, h, w), dim=1)
+            out.append(torch.sum(d.view(1, 81, 2, 1, 1) * 2 ** lvl * s, dim=1))
+        return out
+
+    with torch.no_grad():
+        res["f2_softargmax_L4_r4_cfg2"] = entry(timed(lambda: ops.softargmax(cost, L, r), reps),
+                                                (cost.numel() + L * b * 2 * n) * 4, eager_torch_ms=timed(sam_eager, reps))
+    cg = cost.clone().requires_grad_(True)
+    fl = ops.softargmax(cg, L, r)
+    gfl = [torch.randn_like(f) for f in fl]
+    res["f2_softargmax_backward_L4_r4_cfg2"] = entry(
+        timed(lambda: torch.autograd.grad(fl, cg, gfl, retain_graph=True), reps),
+        (2 * cost.numel() + L * b * 2 * n) * 4)
 
 
 if __name__ == "__main__":
