@@ -201,6 +201,36 @@ int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* fmap2, int 
                                 float* grad_fmap2, void* workspace, void* stream);
 
 /*
+ * Backward warping.  Replaces common.warp.warp_backwards (src/models/common/warp.py:5-33):
+ *   out[b,c,y,x] = mask * bilinear(img2[b,c], x + flow[b,0,y,x], y + flow[b,1,y,x])   (zero padding,
+ *   align_corners=True), mask = (in-bounds bilinear weight > 1 - eps) (grid_sample of ones, :28-30).
+ * img2, out (B, C, h, w); flow (B, 2, h, w); mask (B, h, w) uint8 or NULL (the reference's bool mask is
+ * this plane broadcast over C).  The flow carries no gradient (dicl.py:178 detaches it).
+ */
+int rmd_warp_backwards(const float* img2, const float* flow, int batch, int channels, int height, int width,
+                       float eps, float* out, unsigned char* mask, void* stream);
+
+/* d img2 (B, C, h, w) = bilinear^T(mask * grad_out); zeroes grad_img2 first (float atomics, like ATen). */
+int rmd_warp_backwards_backward(const float* grad_out, const float* flow, int batch, int channels, int height,
+                                int width, float eps, float* grad_img2, void* stream);
+
+/* Bytes of device workspace rmd_dicl_stack_int_warped(_backward) needs (warped map + flags). */
+size_t rmd_dicl_stack_int_warped_workspace_bytes(int batch, int channels, int height, int width);
+
+/*
+ * FlowLevel with a coarse flow (src/models/impls/dicl.py:171-238): feat2 is warped back by `flow`
+ * (warp_backwards, eps 1e-5) and the masked integer volume of rmd_dicl_stack_int is built on it.  The
+ * warp runs inside the occlusion-flag pass, so the volume costs the same launches as without warping.
+ */
+int rmd_dicl_stack_int_warped(const float* fmap1, const float* fmap2, const float* flow, int batch, int channels,
+                              int height, int width, int ru, int rv, float* out, void* workspace, void* stream);
+
+/* Gradients of rmd_dicl_stack_int_warped w.r.t. fmap1 and fmap2 (flow and masks detached). */
+int rmd_dicl_stack_int_warped_backward(const float* grad_mvol, const float* fmap2, const float* flow, int batch,
+                                       int channels, int height, int width, int ru, int rv, float* grad_fmap1,
+                                       float* grad_fmap2, void* workspace, void* stream);
+
+/*
  * Displacement-aware projection: out[b,o,p] = sum_i W[o,i] x[b,i,p] (1x1 conv, no bias) with
  * W = conv1.weight[:,:,0,0] (D x D).  Replaces DisplacementAwareProjection.forward
  * (src/models/common/blocks/dicl.py:143-150), the per-level DAPs of raft.py:146-168 and the

@@ -133,3 +133,49 @@ def dap_backward(x, weight, grad_out):
     gx = np.matmul(wgt.T, g).reshape(x.shape)
     gw = np.einsum("bop,bip->oi", g, xf).reshape(weight.shape)
     return gx, gw
+
+
+def _warp_taps(flow):
+    """Bilinear taps of warp_backwards: positions (x + fx, y + fy) in float32 like the reference's grid + flow."""
+    b, _, h, w = flow.shape
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    ix = (xs[None].astype(np.float32) + flow[:, 0].astype(np.float32)).astype(np.float64)
+    iy = (ys[None].astype(np.float32) + flow[:, 1].astype(np.float32)).astype(np.float64)
+    x0, y0 = np.floor(ix), np.floor(iy)
+    fx, fy = ix - x0, iy - y0
+    taps = []
+    for dy, wy in ((0, 1.0 - fy), (1, fy)):
+        for dx, wx in ((0, 1.0 - fx), (1, fx)):
+            xx, yy = x0.astype(np.int64) + dx, y0.astype(np.int64) + dy
+            inb = (xx >= 0) & (xx < w) & (yy >= 0) & (yy < h)
+            taps.append((np.where(inb, yy * w + xx, 0), np.where(inb, wx * wy, 0.0)))
+    return taps
+
+
+def warp_backwards(img2, flow, eps=1e-5):
+    """common/warp.py:5-33: bilinear sample of img2 at grid + flow (zero padding, align_corners), times
+    the validity mask (in-bounds bilinear weight > 1 - eps).  -> (est * mask (B,C,h,w), mask (B,h,w) bool)."""
+    b, c, h, w = img2.shape
+    flat = img2.reshape(b, c, h * w)
+    est = np.zeros((b, c, h * w))
+    wsum = np.zeros((b, h * w))
+    for idx, wt in _warp_taps(flow):
+        idx, wt = idx.reshape(b, -1), wt.reshape(b, -1)
+        est += np.take_along_axis(flat, np.broadcast_to(idx[:, None], (b, c, h * w)), axis=2) * wt[:, None]
+        wsum += wt
+    mask = wsum > np.float32(1.0 - eps)
+    return (est * mask[:, None]).reshape(b, c, h, w), mask.reshape(b, h, w)
+
+
+def warp_backwards_backward(flow, grad_out, eps=1e-5):
+    """d img2 of warp_backwards (flow and mask carry no gradient, dicl.py:178 detaches the flow)."""
+    b, c, h, w = grad_out.shape
+    _, mask = warp_backwards(np.zeros((b, 1, h, w)), flow, eps)
+    g = grad_out.reshape(b, c, h * w) * mask.reshape(b, 1, h * w)
+    out = np.zeros((b, c, h * w))
+    for idx, wt in _warp_taps(flow):
+        idx, wt = idx.reshape(b, -1), wt.reshape(b, -1)
+        for bi in range(b):
+            for ci in range(c):
+                np.add.at(out[bi, ci], idx[bi], g[bi, ci] * wt[bi])
+    return out.reshape(b, c, h, w)

@@ -584,6 +584,89 @@ int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int
     return RMD_OK;
 }
 
+// ---- backward warping (common/warp.py:5-33), alone or fused into the occlusion pass of the integer
+// volume (impls/dicl.py:178-181 -> 212-238) ---------------------------------------------------------
+// warped[c, p] = mask(p) * bilinear(img2[c], x + fx, y + fy) with zero padding, where mask(p) = the
+// in-bounds bilinear weight > 1 - eps (grid_sample of a ones tensor, warp.py:28-30).  One lane per pixel
+// loops over the channels; with NZ it also writes the occlusion flag sum_c warped[c, p] != 0 that
+// dicl_stack_int_kernel consumes, so the warp costs no extra pass over the warped map.
+struct WarpTaps {
+    int idx[4];
+    float wgt[4];
+    bool valid;
+};
+
+__device__ __forceinline__ WarpTaps warp_taps(const float* __restrict__ flow, int b, int p, int h, int w, float eps) {
+    const int n = h * w;
+    const int y = p / w, x = p - y * w;
+    const float ix = (float)x + flow[((size_t)b * 2 + 0) * n + p];
+    const float iy = (float)y + flow[((size_t)b * 2 + 1) * n + p];
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const float ax = ix - fx0, ay = iy - fy0;
+    WarpTaps t;
+    float wsum = 0.f;
+    // far-away positions: clamp before the int conversion (their taps are all out of bounds anyway)
+    const int x0 = (int)fminf(fmaxf(fx0, -2.f), (float)w + 1.f), y0 = (int)fminf(fmaxf(fy0, -2.f), (float)h + 1.f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dx = k & 1, dy = k >> 1;
+        const int xx = x0 + dx, yy = y0 + dy;
+        const bool in = xx >= 0 && xx < w && yy >= 0 && yy < h;
+        const float wk = (dx ? ax : 1.f - ax) * (dy ? ay : 1.f - ay);
+        t.idx[k] = in ? yy * w + xx : 0;
+        t.wgt[k] = in ? wk : 0.f;
+        wsum += t.wgt[k];
+    }
+    t.valid = wsum > 1.0f - eps;
+    return t;
+}
+
+template <bool NZ>
+__global__ void __launch_bounds__(kThreads)
+warp_kernel(const float* __restrict__ img2, const float* __restrict__ flow, int C, int h, int w, float eps,
+            float* __restrict__ out, unsigned char* __restrict__ mask, unsigned char* __restrict__ nz) {
+    const int n = h * w;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    if (p >= n) return;
+    const WarpTaps t = warp_taps(flow, b, p, h, w, eps);
+    const float* src = img2 + (size_t)b * C * n;
+    float* o = out + (size_t)b * C * n + p;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+        const float* sc = src + (size_t)c * n;
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v = fmaf(t.wgt[k], sc[t.idx[k]], v);
+        v = t.valid ? v : 0.f;
+        o[(size_t)c * n] = v;
+        s += v;
+    }
+    if (mask) mask[(size_t)b * n + p] = t.valid;
+    if (NZ) nz[(size_t)b * n + p] = s != 0.f;
+}
+
+// d img2 += bilinear^T (mask * grad): float atomics onto the 4 taps (as ATen's grid_sampler_2d_backward)
+__global__ void __launch_bounds__(kThreads)
+warp_backward_kernel(const float* __restrict__ grad, const float* __restrict__ flow, int C, int h, int w, float eps,
+                     float* __restrict__ grad_img2) {
+    const int n = h * w;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    if (p >= n) return;
+    const WarpTaps t = warp_taps(flow, b, p, h, w, eps);
+    if (!t.valid) return;
+    const float* g = grad + (size_t)b * C * n + p;
+    float* d = grad_img2 + (size_t)b * C * n;
+    for (int c = 0; c < C; ++c) {
+        const float gv = g[(size_t)c * n];
+        if (gv == 0.f) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (t.wgt[k] != 0.f) atomicAdd(d + (size_t)c * n + t.idx[k], t.wgt[k] * gv);
+    }
+}
+
 }  // namespace
 }  // namespace rmd
 
@@ -706,4 +789,76 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
         dap_kernel<false><<<grid, kThreads, 0, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
     }
     return check_launch("rmd_dap");
+}
+
+extern "C" int rmd_warp_backwards(const float* img2, const float* flow, int batch, int channels, int height,
+                                  int width, float eps, float* out, unsigned char* mask, void* stream) {
+    RMD_REQUIRE(img2 && flow && out, RMD_ERR_ARG, "rmd_warp_backwards: null pointer");
+    RMD_REQUIRE(batch > 0 && batch <= 65535 && channels > 0 && height > 0 && width > 0, RMD_ERR_SHAPE,
+                "rmd_warp_backwards: bad sizes");
+    const int n = height * width;
+    warp_kernel<false><<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, as_stream(stream)>>>(
+        img2, flow, channels, height, width, eps, out, mask, nullptr);
+    return check_launch("rmd_warp_backwards");
+}
+
+extern "C" int rmd_warp_backwards_backward(const float* grad_out, const float* flow, int batch, int channels,
+                                           int height, int width, float eps, float* grad_img2, void* stream) {
+    RMD_REQUIRE(grad_out && flow && grad_img2, RMD_ERR_ARG, "rmd_warp_backwards_backward: null pointer");
+    RMD_REQUIRE(batch > 0 && batch <= 65535 && channels > 0 && height > 0 && width > 0, RMD_ERR_SHAPE,
+                "rmd_warp_backwards_backward: bad sizes");
+    const int n = height * width;
+    hipStream_t st = as_stream(stream);
+    (void)hipMemsetAsync(grad_img2, 0, sizeof(float) * (size_t)batch * channels * n, st);
+    warp_backward_kernel<<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(
+        grad_out, flow, channels, height, width, eps, grad_img2);
+    return check_launch("rmd_warp_backwards_backward");
+}
+
+extern "C" size_t rmd_dicl_stack_int_warped_workspace_bytes(int batch, int channels, int height, int width) {
+    if (batch < 1 || channels < 1 || height < 1 || width < 1) return 0;
+    const size_t n = (size_t)height * width;
+    return ((size_t)batch * channels * n * sizeof(float) + 2 * (size_t)batch * n + 255) & ~(size_t)255;
+}
+
+extern "C" int rmd_dicl_stack_int_warped(const float* fmap1, const float* fmap2, const float* flow, int batch,
+                                         int channels, int height, int width, int ru, int rv, float* out,
+                                         void* workspace, void* stream) {
+    RMD_REQUIRE(fmap1 && fmap2 && flow && out && workspace, RMD_ERR_ARG, "rmd_dicl_stack_int_warped: null pointer");
+    RMD_REQUIRE(batch > 0 && batch <= 65535 && channels > 0 && height > 0 && width > 0 && ru >= 0 && rv >= 0,
+                RMD_ERR_SHAPE, "rmd_dicl_stack_int_warped: bad sizes");
+    RMD_REQUIRE((height * width) % 4 == 0, RMD_ERR_SHAPE, "rmd_dicl_stack_int_warped: h*w must be a multiple of 4");
+    IntParams P{batch, channels, height, width, ru, rv};
+    hipStream_t st = as_stream(stream);
+    const int n = height * width;
+    float* warped = static_cast<float*>(workspace);
+    unsigned char* nz = reinterpret_cast<unsigned char*>(warped + (size_t)batch * channels * n);
+    warp_kernel<true><<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(
+        fmap2, flow, channels, height, width, 1e-5f, warped, nullptr, nz);
+    dim3 grid((n / 4 + kThreads - 1) / kThreads, (2 * ru + 1) * (2 * rv + 1), batch);
+    dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, warped, nz, P, out);
+    return check_launch("rmd_dicl_stack_int_warped");
+}
+
+extern "C" int rmd_dicl_stack_int_warped_backward(const float* grad_mvol, const float* fmap2, const float* flow,
+                                                  int batch, int channels, int height, int width, int ru, int rv,
+                                                  float* grad_fmap1, float* grad_fmap2, void* workspace,
+                                                  void* stream) {
+    RMD_REQUIRE(grad_mvol && fmap2 && flow && grad_fmap1 && grad_fmap2 && workspace, RMD_ERR_ARG,
+                "rmd_dicl_stack_int_warped_backward: null pointer");
+    RMD_REQUIRE(batch > 0 && batch <= 65535 && channels > 0 && height > 0 && width > 0 && ru >= 0 && rv >= 0,
+                RMD_ERR_SHAPE, "rmd_dicl_stack_int_warped_backward: bad sizes");
+    IntParams P{batch, channels, height, width, ru, rv};
+    hipStream_t st = as_stream(stream);
+    const int n = height * width;
+    float* warped = static_cast<float*>(workspace);
+    unsigned char* nz = reinterpret_cast<unsigned char*>(warped + (size_t)batch * channels * n);
+    const dim3 pix((n + kThreads - 1) / kThreads, batch);
+    // recompute the occlusion flags; the warped map's buffer then receives d warped
+    warp_kernel<true><<<pix, kThreads, 0, st>>>(fmap2, flow, channels, height, width, 1e-5f, warped, nullptr, nz);
+    dicl_stack_int_backward_kernel<<<dim3((n + kThreads - 1) / kThreads, channels, batch), kThreads, 0, st>>>(
+        grad_mvol, nz, P, grad_fmap1, warped);
+    (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * n, st);
+    warp_backward_kernel<<<pix, kThreads, 0, st>>>(warped, flow, channels, height, width, 1e-5f, grad_fmap2);
+    return check_launch("rmd_dicl_stack_int_warped_backward");
 }

@@ -8,11 +8,12 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.corr.make_cmod / CorrelationModule <- src/models/common/corr/{dicl,dicl_1x1,dicl_emb,dot}.py
   rmd.raft_dicl_ml.CorrelationModule    <- src/models/impls/raft_dicl_ml.py:235-343
   rmd.blocks.dicl                       <- src/models/common/blocks/dicl.py:93-150
-  rmd.dicl.compute_cost                 <- src/models/impls/dicl.py:212-241
+  rmd.dicl.compute_cost                 <- src/models/impls/dicl.py:171-241 (+ fused warp)
+  rmd.warp.warp_backwards               <- src/models/common/warp.py:5-33
   rmd.raft.Up8Network / SoftArgMax*     <- src/models/impls/raft.py:98-190,299-331 (rmd.heads)
 """
 
-from . import blocks, corr, dicl, heads, ops, raft, raft_dicl_ml, raft_fs  # noqa: F401
+from . import blocks, corr, dicl, heads, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

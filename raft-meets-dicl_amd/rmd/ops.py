@@ -365,6 +365,50 @@ def dicl_stack_int(fmap1, fmap2, ru, rv):
     return _DiclStackInt.apply(fmap1, fmap2, ru, rv)
 
 
+class _DiclStackIntWarped(torch.autograd.Function):
+    """Integer volume on feat2 warped back by a (detached) flow — impls/dicl.py:178-181 + 212-238."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, flow, ru, rv):
+        _require_gpu(f1, f2, flow)
+        f1c = f1.detach().float().contiguous()
+        f2c = f2.detach().float().contiguous()
+        fc = flow.detach().float().contiguous()
+        b, c, h, w = f1c.shape
+        if tuple(f2c.shape) != (b, c, h, w) or tuple(fc.shape) != (b, 2, h, w):
+            raise ValueError("dicl_stack_int_warped: need fmap1, fmap2 (B,C,h,w) and flow (B,2,h,w)")
+        lib = _lib.lib()
+        ws = torch.empty(lib.rmd_dicl_stack_int_warped_workspace_bytes(b, c, h, w), dtype=torch.uint8,
+                         device=f1c.device)
+        out = torch.empty((b, 2 * ru + 1, 2 * rv + 1, 2 * c, h, w), dtype=torch.float32, device=f1c.device)
+        with torch.cuda.device(f1c.device):
+            _lib.check(lib.rmd_dicl_stack_int_warped(_ptr(f1c), _ptr(f2c), _ptr(fc), b, c, h, w, ru, rv, _ptr(out),
+                                                     _ptr(ws), _stream(f1c)), "rmd_dicl_stack_int_warped")
+        ctx.save_for_backward(f2c, fc)
+        ctx.meta = (b, c, h, w, ru, rv)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        f2c, fc = ctx.saved_tensors
+        b, c, h, w, ru, rv = ctx.meta
+        g = grad.float().contiguous()
+        lib = _lib.lib()
+        ws = torch.empty(lib.rmd_dicl_stack_int_warped_workspace_bytes(b, c, h, w), dtype=torch.uint8, device=g.device)
+        g1 = torch.empty((b, c, h, w), dtype=torch.float32, device=g.device)
+        g2 = torch.empty((b, c, h, w), dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            _lib.check(lib.rmd_dicl_stack_int_warped_backward(_ptr(g), _ptr(f2c), _ptr(fc), b, c, h, w, ru, rv,
+                                                              _ptr(g1), _ptr(g2), _ptr(ws), _stream(g)),
+                       "rmd_dicl_stack_int_warped_backward")
+        return g1, g2, None, None, None
+
+
+def dicl_stack_int_warped(fmap1, fmap2, flow, ru, rv):
+    """Masked integer volume of (fmap1, warp_backwards(fmap2, flow)) in one fused pass pair."""
+    return _DiclStackIntWarped.apply(fmap1, fmap2, flow, ru, rv)
+
+
 class _Dap(torch.autograd.Function):
     """out[b,o,p] = sum_i W[o,i] x[b,i,p] — blocks/dicl.py:143-150 (1x1 conv, no bias)."""
 

@@ -14,6 +14,8 @@ The MatchingNet that consumes a6/a8 (MIOpen convolutions, out of scope) is timed
   * f1  on-the-fly lookup (rmd_corr_otf_*) at cfg2: prepare + per-lookup time, bf16 / fp32
   * f2  flow heads at cfg2 (B=8, 55x128): rmd_up8 (+backward), rmd_softargmax L=4 r=4 (+backward),
         each beside the reference's eager torch formulation on the same GPU (raft.py:112-135, 319-331)
+  * f3  warped DICL volume (rmd_dicl_stack_int_warped) at cfg3 level 2 (B=8, C=32, 96x128, ru=rv=3) and
+        rmd_warp_backwards alone, beside the reference's eager warp (warp.py:5-33)
 usage: python tools/bench_components.py [reps] [fs|heads]   -> one JSON document on stdout
       ('fs' runs only the a4 / f1 part, 'heads' only f2)
 """
@@ -225,6 +227,33 @@ def heads(res, reps, dev, g):
     cg = cost.clone().requires_grad_(True)
     fl = ops.softargmax(cg, L, r)
     gfl = [torch.randn_like(f) for f in fl]
+    # f3: warped integer volume, cfg3 level 2
+    from rmd import warp as rwarp
+    bb, c, hh, ww = 8, 32, 96, 128
+    f1 = torch.randn(bb, c, hh, ww, generator=g).to(dev)
+    f2 = torch.randn(bb, c, hh, ww, generator=g).to(dev)
+    fl = (2 * torch.randn(bb, 2, hh, ww, generator=g)).to(dev)
+
+    def warp_eager():                      # warp.py:5-33
+        gx = torch.arange(ww, device=dev).view(1, ww).expand(hh, -1)
+        gy = torch.arange(hh, device=dev).view(hh, 1).expand(-1, ww)
+        fpos = (torch.stack((gx, gy), 0).float() + fl).permute(0, 2, 3, 1)
+        fpos[..., 0] = 2 * fpos[..., 0] / (ww - 1) - 1
+        fpos[..., 1] = 2 * fpos[..., 1] / (hh - 1) - 1
+        est = F.grid_sample(f2, fpos, align_corners=True)
+        m = F.grid_sample(torch.ones(f2.shape, device=dev), fpos, align_corners=True) > (1.0 - 1e-5)
+        return est * m, m
+
+    with torch.no_grad():
+        nbytes = bb * c * hh * ww * 4
+        res["f3_warp_backwards_cfg3_l2"] = entry(timed(lambda: rwarp.warp_backwards(f2, fl), reps),
+                                                 2 * nbytes + fl.numel() * 4 + bb * hh * ww,
+                                                 eager_torch_ms=timed(warp_eager, reps))
+        vol = bb * 49 * 2 * nbytes
+        res["f3_dicl_stack_int_warped_cfg3_l2"] = entry(
+            timed(lambda: ops.dicl_stack_int_warped(f1, f2, fl, 3, 3), reps), vol + 3 * nbytes + fl.numel() * 4,
+            unwarped_ms=timed(lambda: ops.dicl_stack_int(f1, f2, 3, 3), reps),
+            eager_warp_then_rmd_volume_ms=timed(lambda: ops.dicl_stack_int(f1, warp_eager()[0], 3, 3), reps))
     res["f2_softargmax_backward_L4_r4_cfg2"] = entry(
         timed(lambda: torch.autograd.grad(fl, cg, gfl, retain_graph=True), reps),
         (2 * cost.numel() + L * b * 2 * n) * 4)
