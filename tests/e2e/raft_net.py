@@ -154,9 +154,10 @@ class Up8Network(nn.Module):
 
 
 class RaftNet(nn.Module):
-    """RaftModule (raft.py:334-433) at its defaults; `corr_block` is rmd.raft.CorrBlock."""
+    """RaftModule (raft.py:334-433) at its defaults; `corr_block` is rmd.raft.CorrBlock, `upnet_cls`
+    optionally rmd.raft.Up8Network (default: the eager restatement above)."""
 
-    def __init__(self, corr_block, corr_levels=4, corr_radius=4, precision="fp32"):
+    def __init__(self, corr_block, corr_levels=4, corr_radius=4, precision="fp32", upnet_cls=None):
         super().__init__()
         self.corr_block = corr_block
         self.precision = precision
@@ -164,7 +165,7 @@ class RaftNet(nn.Module):
         self.fnet = FeatureEncoder(256, "instance")
         self.cnet = FeatureEncoder(256, "batch")
         self.update_block = BasicUpdateBlock(corr_levels * (2 * corr_radius + 1) ** 2)
-        self.upnet = Up8Network(128)
+        self.upnet = (upnet_cls or Up8Network)(128)     # rmd.raft.Up8Network: the HIP convex upsampling
 
     def forward(self, img1, img2, iterations=12):
         fmap1, fmap2 = self.fnet(img1).float(), self.fnet(img2).float()

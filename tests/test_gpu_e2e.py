@@ -6,7 +6,8 @@ reference model's mean EPE after every iteration and its flow at 4096 fixed pixe
 iterations 1, 4 and 12, for name-keyed deterministic weights (detinit.det_init_fanin) and the
 synthetic pair of synth.frame_pair (known constant flow).  tests/e2e/raft_net.py restates the
 network with the reference's module names (verified bitwise against the reference on CPU when given
-the reference's CorrBlock); here its correlation is rmd.raft.CorrBlock on the GPU.
+the reference's CorrBlock); here its correlation is rmd.raft.CorrBlock and its convex upsampling
+rmd.raft.Up8Network (rmd_up8), both on the GPU.
 
 Tolerances: |EPE - EPE_ref| <= 1e-3 px after every iteration (north_star) in both precision modes;
 sampled flow max |d| <= 1e-2 px (fp32 mode: MIOpen convolutions vs CPU ATen differ in summation
@@ -37,7 +38,8 @@ def test_raft_12_iterations_epe_matches_reference(precision):
     torch.backends.cuda.matmul.allow_tf32 = False
     g = load_golden("e2e_raft_436x1024")
     h, w, iters = int(g["height"]), int(g["width"]), int(g["iterations"])
-    net = det_init_fanin(RaftNet(rmd.raft.CorrBlock, precision=precision)).eval().cuda()
+    net = det_init_fanin(RaftNet(rmd.raft.CorrBlock, precision=precision,
+                                 upnet_cls=rmd.raft.Up8Network)).eval().cuda()
     assert sorted(net.state_dict().keys()) == sorted(g["keys"].tolist())
     img1, img2, gt = frame_pair(h, w)
     with torch.no_grad():

@@ -232,12 +232,12 @@ def heads(res, reps, dev, g):
     bb, c, hh, ww = 8, 32, 96, 128
     f1 = torch.randn(bb, c, hh, ww, generator=g).to(dev)
     f2 = torch.randn(bb, c, hh, ww, generator=g).to(dev)
-    fl = (2 * torch.randn(bb, 2, hh, ww, generator=g)).to(dev)
+    wfl = (2 * torch.randn(bb, 2, hh, ww, generator=g)).to(dev)
 
     def warp_eager():                      # warp.py:5-33
         gx = torch.arange(ww, device=dev).view(1, ww).expand(hh, -1)
         gy = torch.arange(hh, device=dev).view(hh, 1).expand(-1, ww)
-        fpos = (torch.stack((gx, gy), 0).float() + fl).permute(0, 2, 3, 1)
+        fpos = (torch.stack((gx, gy), 0).float() + wfl).permute(0, 2, 3, 1)
         fpos[..., 0] = 2 * fpos[..., 0] / (ww - 1) - 1
         fpos[..., 1] = 2 * fpos[..., 1] / (hh - 1) - 1
         est = F.grid_sample(f2, fpos, align_corners=True)
@@ -246,12 +246,12 @@ def heads(res, reps, dev, g):
 
     with torch.no_grad():
         nbytes = bb * c * hh * ww * 4
-        res["f3_warp_backwards_cfg3_l2"] = entry(timed(lambda: rwarp.warp_backwards(f2, fl), reps),
-                                                 2 * nbytes + fl.numel() * 4 + bb * hh * ww,
+        res["f3_warp_backwards_cfg3_l2"] = entry(timed(lambda: rwarp.warp_backwards(f2, wfl), reps),
+                                                 2 * nbytes + wfl.numel() * 4 + bb * hh * ww,
                                                  eager_torch_ms=timed(warp_eager, reps))
-        vol = bb * 49 * 2 * nbytes
+        vol = 49 * 2 * nbytes                # (B, 7, 7, 2C, h, w) fp32
         res["f3_dicl_stack_int_warped_cfg3_l2"] = entry(
-            timed(lambda: ops.dicl_stack_int_warped(f1, f2, fl, 3, 3), reps), vol + 3 * nbytes + fl.numel() * 4,
+            timed(lambda: ops.dicl_stack_int_warped(f1, f2, wfl, 3, 3), reps), vol + 3 * nbytes + wfl.numel() * 4,
             unwarped_ms=timed(lambda: ops.dicl_stack_int(f1, f2, 3, 3), reps),
             eager_warp_then_rmd_volume_ms=timed(lambda: ops.dicl_stack_int(f1, warp_eager()[0], 3, 3), reps))
     res["f2_softargmax_backward_L4_r4_cfg2"] = entry(
