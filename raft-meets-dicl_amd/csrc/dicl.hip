@@ -16,6 +16,7 @@
 
 #include "rmd_common.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -388,6 +389,118 @@ dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __r
     }
 }
 
+// Separable form of the general backward (scaled grids with 0 <= sx, sy <= 1, raft_dicl_ml levels > 0).
+// The x-weights of displacement (a, bb) depend on a only and the y-weights on bb only, so a lane's 81
+// f2-half gradients reach a K x K patch as  patch[j][i] = sum_bb wy_bb(j) * sum_a wx_a(i) * g[a][bb]:
+// K FMAs per displacement plus K^2 per row bb, all in registers, then K^2 window atomics per lane
+// instead of 4 per displacement (324 for r = 4).  A lane whose taps do not fit the patch (fp32
+// rounding at an exact span bound) takes the per-tap path, so the result never depends on K.
+template <int K>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                               float* __restrict__ gf1, float* __restrict__ gf2) {
+    __shared__ float win[kWinFloats];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p < n;
+    const int d = 2 * P.radius + 1;
+    float cxs = 0.f, cys = 0.f;
+    if (pv) {
+        cxs = fminf(fmaxf(coords[(size_t)b * 2 * n + p] * P.inv_scale, -1.0e6f), 1.0e6f);
+        cys = fminf(fmaxf(coords[(size_t)b * 2 * n + n + p] * P.inv_scale, -1.0e6f), 1.0e6f);
+    }
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    const float py0 = (cys - (float)P.radius) * P.sy, px0 = (cxs - (float)P.radius) * P.sx;
+    const int ybase = (int)floorf(py0), xbase = (int)floorf(px0);
+    if (pv) atomicMin(&wmin, min(max(ybase, 0), P.hl));
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    if (pv) {
+        const float* gp = g + (size_t)b * d * d * dstride + p;
+        // does every tap land inside the K x K patch?
+        const float pxl = (cxs + (float)P.radius) * P.sx, pyl = (cys + (float)P.radius) * P.sy;
+        const bool fits = (int)floorf(pxl) - xbase <= K - 2 && (int)floorf(pyl) - ybase <= K - 2;
+        float s1 = 0.f;
+        if (fits) {
+            float patch[K][K];
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) patch[j][i] = 0.f;
+            for (int bb = 0; bb < d; ++bb) {
+                float row[K];
+#pragma unroll
+                for (int i = 0; i < K; ++i) row[i] = 0.f;
+                for (int a = 0; a < d; ++a) {
+                    const float* gd = gp + (size_t)(a * d + bb) * dstride;
+                    s1 += gd[(size_t)c * n];
+                    const float gv = gd[(size_t)(C + c) * n];
+                    const float px = (cxs + (float)(a - P.radius)) * P.sx;
+                    const float fx0 = floorf(px);
+                    const int rx = (int)fx0 - xbase;
+                    const float w1 = (px - fx0) * gv, w0 = gv - w1;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) row[i] += i == rx ? w0 : (i == rx + 1 ? w1 : 0.f);
+                }
+                const float py = (cys + (float)(bb - P.radius)) * P.sy;
+                const float fy0 = floorf(py);
+                const int ry = (int)fy0 - ybase;
+                const float fy = py - fy0;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const float wy = j == ry ? 1.f - fy : (j == ry + 1 ? fy : 0.f);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) patch[j][i] = fmaf(wy, row[i], patch[j][i]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const int yy = ybase + j;
+                if (yy < 0 || yy >= P.hl) continue;
+                const bool in_win = yy >= wy0 && yy - wy0 < wrows;
+                float* r = in_win ? win + (size_t)(yy - wy0) * P.wl : g2c + (size_t)yy * P.wl;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const int xx = xbase + i;
+                    if (xx >= 0 && xx < P.wl && patch[j][i] != 0.f) atomicAdd(r + xx, patch[j][i]);
+                }
+            }
+        } else {
+            for (int a = 0; a < d; ++a) {
+                for (int bb = 0; bb < d; ++bb) {
+                    const float* gd = gp + (size_t)(a * d + bb) * dstride;
+                    s1 += gd[(size_t)c * n];
+                    const float gv = gd[(size_t)(C + c) * n];
+                    const Taps t = make_taps((cxs + (float)(a - P.radius)) * P.sx, (cys + (float)(bb - P.radius)) * P.sy,
+                                             P.hl, P.wl);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (t.wgt[k] == 0.f) continue;
+                        const int yy = t.idx[k] / P.wl;
+                        float* dst = (yy >= wy0 && yy - wy0 < wrows) ? win + (t.idx[k] - wy0 * P.wl) : g2c + t.idx[k];
+                        atomicAdd(dst, gv * t.wgt[k]);
+                    }
+                }
+            }
+        }
+        gf1[((size_t)b * C + c) * n + p] = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
+    }
+}
+
 // ---- DICL baseline integer volume ------------------------------------------------------------
 struct IntParams {
     int B, C, h, w, ru, rv;
@@ -717,6 +830,19 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
         return check_launch("rmd_dicl_stack_backward/patch");
     }
     (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
+    if (level_width <= kWinFloats && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sy >= 0.f && P.sx >= 0.f &&
+        P.sx <= 1.f && P.sy <= 1.f) {
+        // patch edge: floor(span) + 1 tap offsets + 1 for the right/bottom tap + 1 for fp32 rounding, even
+        const float span = 2.0f * radius * std::max(P.sx, P.sy);
+        const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
+        dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        switch (k) {
+#define RMD_KCASE(KK) case KK: dicl_stack_sep_backward_kernel<KK><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); return check_launch("rmd_dicl_stack_backward/separable");
+            RMD_KCASE(4) RMD_KCASE(6) RMD_KCASE(8) RMD_KCASE(10)
+#undef RMD_KCASE
+            default: break;
+        }
+    }
     if (level_width <= kWinFloats && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sy >= 0.f) {
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
         dicl_stack_general_backward_kernel<<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
