@@ -192,7 +192,7 @@ def main():
                 pmc = json.load(fh).get(args.precision, {})
         except (OSError, ValueError):
             pmc = {}
-    roof_gemm = {"kernel": "corr_pyramid_stationary (MFMA GEMM + fused pooled-pyramid epilogue)",
+    roof_gemm = {"kernel": "corr_pyramid_w8 (bf16 MFMA GEMM + fused pooled-pyramid epilogue)",
                  "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
                  "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
