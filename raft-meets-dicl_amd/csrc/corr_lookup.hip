@@ -23,24 +23,33 @@ namespace {
 
 constexpr int kThreads = 256;
 
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 template <int NB> struct Chunk;
 template <> struct Chunk<4> { using T = unsigned; };
-template <> struct Chunk<8> { using T = uint2; };
-template <> struct Chunk<16> { using T = uint4; };
+template <> struct Chunk<8> { using T = u32x2; };
+template <> struct Chunk<16> { using T = u32x4; };
 
-template <int NW>
+// NT (A/B knob RMD_LOOKUP_NT): bit 0 = non-temporal output stores, bit 1 = non-temporal pyramid loads
+template <int NT, typename V>
+__device__ __forceinline__ V ld(const V* p) {
+    if constexpr ((NT & 2) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int NW, int NT>
 __device__ __forceinline__ void load_words(unsigned (&dst)[NW], int at, const unsigned char* src) {
     // NW words (4, 8, 16 or 32 bytes) from a 4/8/16-byte aligned address
     constexpr int NB = NW * 4;
     if constexpr (NB <= 16) {
-        typename Chunk<NB>::T v = *reinterpret_cast<const typename Chunk<NB>::T*>(src);
+        typename Chunk<NB>::T v = ld<NT>(reinterpret_cast<const typename Chunk<NB>::T*>(src));
         const unsigned* u = reinterpret_cast<const unsigned*>(&v);
 #pragma unroll
         for (int i = 0; i < NW; ++i) dst[at + i] = u[i];
     } else {
 #pragma unroll
         for (int k = 0; k < NB / 16; ++k) {
-            uint4 v = reinterpret_cast<const uint4*>(src)[k];
+            u32x4 v = ld<NT>(reinterpret_cast<const u32x4*>(src) + k);
             dst[at + 4 * k + 0] = v.x;
             dst[at + 4 * k + 1] = v.y;
             dst[at + 4 * k + 2] = v.z;
@@ -60,7 +69,7 @@ template <> __device__ __forceinline__ float word_elem<__half>(unsigned w, int i
 // chunks a row can span are fetched from clamped addresses (an unneeded chunk re-reads chunk 0's
 // line) and everything outside the level is zeroed with selects, so all loads of a patch issue
 // back to back.
-template <typename T, int R, int TW>
+template <typename T, int R, int TW, int NT>
 __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long long tile_stride, int tiles_x, int xs,
                                          int lw, bool row_ok, float (&v)[2 * R + 2]) {
     constexpr int S = sizeof(T);
@@ -80,7 +89,7 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
         const bool need = tc >= 0 && tc < tiles_x && c * TW < sh + K;
         const T* p = row_ptr + (long long)(need ? tc : tcl) * tile_stride;
         unsigned tmp[CW];
-        load_words<CW>(tmp, 0, reinterpret_cast<const unsigned char*>(p));
+        load_words<CW, NT>(tmp, 0, reinterpret_cast<const unsigned char*>(p));
 #pragma unroll
         for (int i = 0; i < CW; ++i) wd[c * CW + i] = need ? tmp[i] : 0u;
     }
@@ -109,7 +118,7 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
 
 // ABL (diagnostic, RMD_ABLATE env, fp16/r=4 only): 0 normal, 1 = outputs to one channel slot
 // (no output HBM traffic), 2 = no pyramid loads (zero patch)
-template <typename T, int R, int L, int ABL = 0>
+template <typename T, int R, int L, int ABL = 0, int NT = 0>
 __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const PyrGeom& g, int b, int p, int N,
                                              float x, float y, unsigned zmask, float* __restrict__ o,
                                              bool active) {
@@ -152,7 +161,7 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
 #pragma unroll
             for (int k = 0; k < K; ++k) v[k] = fx * (float)k;
         } else {
-            load_row<T, R, CW>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
+            load_row<T, R, CW, NT>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
         }
         float hcur[D];
 #pragma unroll
@@ -160,7 +169,12 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
         if (j > 0 && active) {
             const int bb = j - 1;
 #pragma unroll
-            for (int a = 0; a < D; ++a) o[ABL == 1 ? 0 : (size_t)(a * D + bb) * N] = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
+            for (int a = 0; a < D; ++a) {
+                float* dst = o + (ABL == 1 ? 0 : (size_t)(a * D + bb) * N);
+                const float val = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
+                if constexpr ((NT & 1) != 0) __builtin_nontemporal_store(val, dst);
+                else *dst = val;
+            }
         }
 #pragma unroll
         for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
@@ -168,7 +182,7 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
 }
 
 // grid: (query blocks, batch, level) — one lane per (query, level)
-template <typename T, int R, int ABL = 0>
+template <typename T, int R, int ABL = 0, int NT = 0>
 __global__ void __launch_bounds__(kThreads)
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
@@ -183,10 +197,10 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     constexpr int D = 2 * R + 1;
     float* o = out + ((size_t)b * g.levels + L) * D * D * N + pc;
     switch (L) {
-        case 0: lookup_level<T, R, 0, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        case 1: lookup_level<T, R, 1, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        case 2: lookup_level<T, R, 2, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        default: lookup_level<T, R, 3, ABL>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 0: lookup_level<T, R, 0, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 1: lookup_level<T, R, 1, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 2: lookup_level<T, R, 2, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        default: lookup_level<T, R, 3, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
     }
 }
 
@@ -203,8 +217,19 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
         if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
         if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
     }
+    // RMD_LOOKUP_NT (A/B, tools/lookup_ab.py): 0 plain, 1 (default) non-temporal output stores,
+    // 2 nt pyramid loads, 3 both.  cfg2 (profiles/lookup_ab_r01.json): 27.1 / 24.4 / 36.6 / 36.8 us —
+    // the 73 MB output is written once and must not evict the pyramid lines that neighbouring
+    // queries' row chunks re-read; nt loads lose exactly that reuse.
+    const char* nt_env = getenv("RMD_LOOKUP_NT");
+    const int nt = nt_env ? atoi(nt_env) : 1;
+    if (radius == 4 && nt == 2) { corr_lookup_kernel<T, 4, 0, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+    if (radius == 4 && nt == 3) { corr_lookup_kernel<T, 4, 0, 3><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
     switch (radius) {
-#define RMD_CASE(RR) case RR: corr_lookup_kernel<T, RR><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); break;
+#define RMD_CASE(RR) case RR: \
+        if (nt == 0) corr_lookup_kernel<T, RR, 0, 0><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        else corr_lookup_kernel<T, RR, 0, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE
         default:

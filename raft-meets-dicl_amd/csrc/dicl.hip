@@ -148,6 +148,14 @@ dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__
     }
 }
 
+typedef __attribute__((ext_vector_type(4))) float f4_t;
+
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(p));
+    else *reinterpret_cast<f4_t*>(p) = v;
+}
+
 // ---- unit-step fast path ---------------------------------------------------------------------
 // When the sample grid has unit steps (sx = sy = 1: corr/dicl.py and every same-size call), the
 // (2r+1)^2 displacements of pixel p sample (x_p + a - r, y_p + b - r) with ONE fractional weight
@@ -155,21 +163,36 @@ dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__
 // (as the RAFT lookup).  One lane per pixel, all displacements, a loop over channels: per channel
 // the patch is read once (instead of 4 taps x (2r+1)^2 gathers), interpolated separably (x, then y)
 // and the (2r+1)^2 f2 values plus the f1 copies are stored as coalesced 256-B wave rows.
-template <int R>
+template <int PX> struct FVec;
+template <> struct FVec<4> { typedef __attribute__((ext_vector_type(4))) float T; };
+template <> struct FVec<2> { typedef __attribute__((ext_vector_type(2))) float T; };
+
+template <bool NT, typename V>
+__device__ __forceinline__ void stv(float* p, V v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<V*>(p));
+    else *reinterpret_cast<V*>(p) = v;
+}
+
+template <int R, int PX, bool NT>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
-                        StackParams P, float* __restrict__ out) {
-    // 4 consecutive pixels per lane (each with its own patch) so every store is a float4 (1 KiB
-    // per wave-instruction); one channel per thread: grid (pixels/1024, C, B)
+                        StackParams P, int nxb, int remap, float* __restrict__ out) {
+    // PX consecutive pixels per lane (each with its own patch) so every store is a PX-float vector
+    // (PX * 256 B per wave-instruction); one channel per thread: 1-D grid of (pixels / 256 PX) x C x B
+    // blocks, remapped so an XCD works on one batch image (its f2 stays in that XCD's L2).  PX = 2
+    // keeps the two interpolated rows of r = 3, 4 in ~100 VGPRs (4 waves per SIMD); PX = 4 needs ~200.
+    typedef typename FVec<PX>::T V;
     constexpr int D = 2 * R + 1, K = 2 * R + 2;
     const int n = P.h * P.w, nl = P.hl * P.wl;
-    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * 4;
-    const int c = blockIdx.y, b = blockIdx.z;
+    const int lid = remap ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int xb = lid % nxb, rest = lid / nxb;
+    const int c = rest % P.C, b = rest / P.C;
+    const int p0 = (xb * kThreads + threadIdx.x) * PX;
     if (p0 >= n) return;
-    float fx[4], fy[4];
-    int xs[4], ys[4];
+    float fx[PX], fy[PX];
+    int xs[PX], ys[PX];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < PX; ++k) {
         float cx = coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale;
         float cy = coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale;
         cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
@@ -183,22 +206,28 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
     const int C = P.C, C2 = 2 * C + P.extra;
     const size_t dstride = (size_t)C2 * n;                       // next displacement plane
     float* o = out + (size_t)b * D * D * dstride + p0;
-    const float4 v1 = *reinterpret_cast<const float4*>(f1 + ((size_t)b * C + c) * n + p0);
+    // stores: wave-uniform plane base + one 32-bit lane offset (saddr + voffset addressing; the
+    // host checks that a batch image's volume stays below 4 GiB), so the 2 D^2 store addresses
+    // cost no VGPRs
+    float* const ob = out + (size_t)b * D * D * dstride;
+    const unsigned lo1 = (unsigned)(((size_t)c * n + p0) * sizeof(float));
+    const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
+    const V v1 = *reinterpret_cast<const V*>(f1 + ((size_t)b * C + c) * n + p0);
     const float* f2c = f2 + ((size_t)b * C + c) * nl;
-    float hprev[4][D];
+    float hprev[PX][D];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        float hcur[4][D];
+        float hcur[PX][D];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < PX; ++k) {
             const int yy = ys[k] + j;
             const bool rok = yy >= 0 && yy < P.hl;
-            const float* row = f2c + (size_t)min(max(yy, 0), P.hl - 1) * P.wl;
+            const unsigned roff = (unsigned)(min(max(yy, 0), P.hl - 1) * P.wl);
             float v[K];
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 const int xx = xs[k] + i;
-                const float e = row[min(max(xx, 0), P.wl - 1)];
+                const float e = f2c[roff + (unsigned)min(max(xx, 0), P.wl - 1)];
                 v[i] = (rok && xx >= 0 && xx < P.wl) ? e : 0.f;
             }
 #pragma unroll
@@ -208,18 +237,16 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
             const int bb = j - 1;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                float* od = o + (size_t)(a * D + bb) * dstride;
-                *reinterpret_cast<float4*>(od + (size_t)c * n) = v1;
-                float4 r;
-                r.x = fmaf(fy[0], hcur[0][a] - hprev[0][a], hprev[0][a]);
-                r.y = fmaf(fy[1], hcur[1][a] - hprev[1][a], hprev[1][a]);
-                r.z = fmaf(fy[2], hcur[2][a] - hprev[2][a], hprev[2][a]);
-                r.w = fmaf(fy[3], hcur[3][a] - hprev[3][a], hprev[3][a]);
-                *reinterpret_cast<float4*>(od + (size_t)(C + c) * n) = r;
+                char* od = reinterpret_cast<char*>(ob + (size_t)(a * D + bb) * dstride);
+                stv<NT>(reinterpret_cast<float*>(od + lo1), v1);
+                V r;
+#pragma unroll
+                for (int k = 0; k < PX; ++k) r[k] = fmaf(fy[k], hcur[k][a] - hprev[k][a], hprev[k][a]);
+                stv<NT>(reinterpret_cast<float*>(od + lo2), r);
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < PX; ++k)
 #pragma unroll
             for (int a = 0; a < D; ++a) hprev[k][a] = hcur[k][a];
     }
@@ -230,8 +257,8 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
             for (int bb = 0; bb < D; ++bb) {
                 float* od = o + (size_t)(a * D + bb) * dstride;
                 const float dx = (float)(a - R), dy = (float)(bb - R);
-                *reinterpret_cast<float4*>(od + (size_t)(2 * C) * n) = make_float4(dx, dx, dx, dx);
-                *reinterpret_cast<float4*>(od + (size_t)(2 * C + 1) * n) = make_float4(dy, dy, dy, dy);
+                *reinterpret_cast<V*>(od + (size_t)(2 * C) * n) = V(dx);
+                *reinterpret_cast<V*>(od + (size_t)(2 * C + 1) * n) = V(dy);
             }
     }
 }
@@ -559,6 +586,90 @@ dicl_stack_int_kernel(const float* __restrict__ f1, const float* __restrict__ f2
     }
 }
 
+// Same output as dicl_stack_int_kernel, restructured for the write stream: a 1-D grid remapped per
+// XCD (one batch image's f1/f2 — 2 x 1.5 MB at cfg3 level 2 — stay in that XCD's L2 while its 49
+// displacement planes re-read them), the channel loop unrolled by U so a lane's loads of U channels
+// are all in flight before its 2U stores, and optionally non-temporal stores (the 1.2 GB volume is
+// written once and read by the next kernel, never by this one).
+template <int CT, bool NT>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_int_v2_kernel(const float* __restrict__ f1, const float* __restrict__ f2,
+                         const unsigned char* __restrict__ nz, IntParams P, int nqb, int remap,
+                         float* __restrict__ out) {
+    constexpr int U = 8;
+    const int n = P.h * P.w;
+    const int dv = 2 * P.rv + 1, ndisp = (2 * P.ru + 1) * dv;
+    const int lid = remap ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int xb = lid % nqb, rest = lid / nqb;
+    const int disp = rest % ndisp, b = rest / ndisp;
+    const int p0 = (xb * kThreads + threadIdx.x) * 4;
+    if (p0 >= n) return;
+    const int i = disp / dv, jj = disp - i * dv;
+    const int di = i - P.ru, dj = jj - P.rv;
+    int src[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = p0 + k;
+        const int y = p / P.w, x = p - y * P.w;
+        const int xx = x + di, yy = y + dj;
+        const bool inb = xx >= 0 && xx < P.w && yy >= 0 && yy < P.h;
+        src[k] = inb ? yy * P.w + xx : 0;
+        ok[k] = inb && nz[(size_t)b * n + src[k]];
+    }
+    const int C = CT ? CT : P.C;
+    float* o = out + ((size_t)(b * ndisp + disp) * 2 * C) * n + p0;
+    const float* f1b = f1 + (size_t)b * C * n + p0;
+    const float* f2b = f2 + (size_t)b * C * n;
+#pragma unroll 4
+    for (int c0 = 0; c0 < C; c0 += U) {
+        f4_t a[U], v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (CT || c0 + u < C) {
+                const float* f2c = f2b + (size_t)(c0 + u) * n;
+                a[u] = *reinterpret_cast<const f4_t*>(f1b + (size_t)(c0 + u) * n);
+                v[u] = f4_t{f2c[src[0]], f2c[src[1]], f2c[src[2]], f2c[src[3]]};
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (CT || c0 + u < C) {
+                const f4_t m1{ok[0] ? a[u].x : 0.f, ok[1] ? a[u].y : 0.f, ok[2] ? a[u].z : 0.f, ok[3] ? a[u].w : 0.f};
+                const f4_t m2{ok[0] ? v[u].x : 0.f, ok[1] ? v[u].y : 0.f, ok[2] ? v[u].z : 0.f, ok[3] ? v[u].w : 0.f};
+                st4<NT>(o + (size_t)(c0 + u) * n, m1);
+                st4<NT>(o + (size_t)(C + c0 + u) * n, m2);
+            }
+        }
+    }
+}
+
+// launch the integer volume (nz already computed); RMD_DICL_INT selects a variant for A/B runs
+// (tools/dicl_ab.py): 1 = the first kernel, 2 = plain stores, 3 = XCD remap.  Measured at cfg3
+// (profiles/dicl_ab_r01.json): 0.366 ms (first) -> 0.234 ms (default: unrolled, nt, no remap)
+int launch_stack_int(const float* fmap1, const float* fmap2, const unsigned char* nz, const IntParams& P,
+                     float* out, hipStream_t st) {
+    const int n = P.h * P.w;
+    const int ndisp = (2 * P.ru + 1) * (2 * P.rv + 1);
+    const int var = env_variant("RMD_DICL_INT");
+    if (var == 1) {          // the first formulation (3-D grid, rolled channel loop)
+        dim3 grid((n / 4 + kThreads - 1) / kThreads, ndisp, P.B);
+        dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, fmap2, nz, P, out);
+        return check_launch("rmd_dicl_stack_int");
+    }
+    const int nqb = (n / 4 + kThreads - 1) / kThreads;
+    const long long nwg = (long long)nqb * ndisp * P.B;
+    RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack_int: grid too large");
+    const bool nt = var != 2, remap = var == 3;
+    if (P.C == 32) {
+        if (nt) dicl_stack_int_v2_kernel<32, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+        else dicl_stack_int_v2_kernel<32, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+    } else {
+        dicl_stack_int_v2_kernel<0, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+    }
+    return check_launch("rmd_dicl_stack_int");
+}
+
 // backward (deterministic gathers, no atomics):
 //   grad_f1[c, p] = sum_{i,j} ok_ij(p) g[i,j,c,p];   grad_f2[c, q] = sum_{i,j} ok_ij(q-d_ij) g[i,j,C+c,q-d_ij]
 __global__ void __launch_bounds__(kThreads)
@@ -794,10 +905,24 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
                           norm_width, extra_delta);
     if (rc) return rc;
     const int d = 2 * radius + 1;
-    if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
-        dim3 grid((height * width / 4 + kThreads - 1) / kThreads, channels, batch);
+    const double image_bytes = 4.0 * d * d * (2.0 * channels + P.extra) * height * width;
+    if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4 && image_bytes < 4294967296.0) {
+        // RMD_DICL_PATCH (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = XCD remap, 3 = 4 pixels per lane.
+        // Measured at cfg4 (profiles/dicl_ab_r01.json): non-temporal stores are the win (0.33 -> 0.26 ms);
+        // the XCD remap does not help (f2 re-reads hit the MALL either way)
+        const int var = env_variant("RMD_DICL_PATCH");
+        const int px = var == 3 ? 4 : 2;
+        const int nxb = (height * width / px + kThreads - 1) / kThreads;
+        const long long nwg = (long long)nxb * channels * batch;
+        RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack: grid too large");
+        const int remap = var == 2;
+        hipStream_t st = as_stream(stream);
         switch (radius) {
-#define RMD_CASE(RR) case RR: dicl_stack_patch_kernel<RR><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out); break;
+#define RMD_CASE(RR) case RR: \
+            if (var == 1) dicl_stack_patch_kernel<RR, 2, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            else if (var == 3) dicl_stack_patch_kernel<RR, 4, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            else dicl_stack_patch_kernel<RR, 2, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            break;
             RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE
         }
@@ -870,9 +995,7 @@ extern "C" int rmd_dicl_stack_int(const float* fmap1, const float* fmap2, int ba
     const int n = height * width;
     unsigned char* nz = reinterpret_cast<unsigned char*>(workspace);
     dicl_nz_kernel<<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(fmap2, P, nz);
-    dim3 grid((n / 4 + kThreads - 1) / kThreads, (2 * ru + 1) * (2 * rv + 1), batch);
-    dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, fmap2, nz, P, out);
-    return check_launch("rmd_dicl_stack_int");
+    return launch_stack_int(fmap1, fmap2, nz, P, out, st);
 }
 
 extern "C" int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* fmap2, int batch, int channels,
@@ -961,9 +1084,8 @@ extern "C" int rmd_dicl_stack_int_warped(const float* fmap1, const float* fmap2,
     unsigned char* nz = reinterpret_cast<unsigned char*>(warped + (size_t)batch * channels * n);
     warp_kernel<true><<<dim3((n + kThreads - 1) / kThreads, batch), kThreads, 0, st>>>(
         fmap2, flow, channels, height, width, 1e-5f, warped, nullptr, nz);
-    dim3 grid((n / 4 + kThreads - 1) / kThreads, (2 * ru + 1) * (2 * rv + 1), batch);
-    dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, warped, nz, P, out);
-    return check_launch("rmd_dicl_stack_int_warped");
+    const int rc = launch_stack_int(fmap1, warped, nz, P, out, st);
+    return rc ? rc : check_launch("rmd_dicl_stack_int_warped");
 }
 
 extern "C" int rmd_dicl_stack_int_warped_backward(const float* grad_mvol, const float* fmap2, const float* flow,

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "rmd.h"
 
@@ -66,6 +67,21 @@ inline PyrGeom make_geom(const rmd_pyramid_desc& d) {
 __host__ __device__ constexpr int level_chunk(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// XCD-aware block order: the dispatcher deals workgroups of a 1-D grid round-robin over the 8 XCDs
+// (block i -> XCD i mod 8); remap so that XCD k runs the k-th contiguous eighth of the logical
+// block range, keeping what consecutive logical blocks share (one batch image's feature maps) in
+// that XCD's own L2.
+__device__ __forceinline__ int xcd_block(int orig, int nwg) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// diagnostic variant selector for A/B runs (env RMD_<NAME>, default 0); read on the host per launch
+inline int env_variant(const char* name) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : 0;
+}
 
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
