@@ -58,7 +58,18 @@ struct StackParams {
     float sx, sy;                               // (wl-1)/(wn-1), (hl-1)/(hn-1)
 };
 
-// grid: (pixel quads, d*d, B); one lane = 4 consecutive pixels of one displacement plane
+typedef __attribute__((ext_vector_type(4))) float f4_t;
+
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(p));
+    else *reinterpret_cast<f4_t*>(p) = v;
+}
+
+// grid: (pixel quads, d*d, B); one lane = 4 consecutive pixels of one displacement plane.  The
+// channel loop is unrolled by U so a lane's f1 row loads and 16 U bilinear taps are in flight
+// before its 2 U stores; stores are non-temporal (the volume is written once, read by MatchingNet).
+template <bool NT, int U>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_kernel(const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
                   StackParams P, float* __restrict__ out) {
@@ -84,15 +95,26 @@ dicl_stack_kernel(const float* __restrict__ f1, const float* __restrict__ f2, co
     float* o = out + ((size_t)(b * d * d + disp) * C2) * n + p0;
     const float* f1b = f1 + (size_t)b * C * n + p0;
     const float* f2b = f2 + (size_t)b * C * nl;
-    for (int c = 0; c < C; ++c) {
-        *reinterpret_cast<float4*>(o + (size_t)c * n) = *reinterpret_cast<const float4*>(f1b + (size_t)c * n);
-        const float* f2c = f2b + (size_t)c * nl;
-        float v[4];
+    for (int c0 = 0; c0 < C; c0 += U) {
+        f4_t a1[U], v2[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            v[k] = t[k].wgt[0] * f2c[t[k].idx[0]] + t[k].wgt[1] * f2c[t[k].idx[1]] +
-                   t[k].wgt[2] * f2c[t[k].idx[2]] + t[k].wgt[3] * f2c[t[k].idx[3]];
-        *reinterpret_cast<float4*>(o + (size_t)(C + c) * n) = make_float4(v[0], v[1], v[2], v[3]);
+        for (int u = 0; u < U; ++u) {
+            if (c0 + u < C) {
+                const float* f2c = f2b + (size_t)(c0 + u) * nl;
+                a1[u] = *reinterpret_cast<const f4_t*>(f1b + (size_t)(c0 + u) * n);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v2[u][k] = t[k].wgt[0] * f2c[t[k].idx[0]] + t[k].wgt[1] * f2c[t[k].idx[1]] +
+                               t[k].wgt[2] * f2c[t[k].idx[2]] + t[k].wgt[3] * f2c[t[k].idx[3]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (c0 + u < C) {
+                st4<NT>(o + (size_t)(c0 + u) * n, a1[u]);
+                st4<NT>(o + (size_t)(C + c0 + u) * n, v2[u]);
+            }
+        }
     }
     if (P.extra) {       // dicl_emb.py:81-85: delta (dx = a-r, dy = bb-r) as two constant channels
         const float dx = (float)(a - P.radius), dy = (float)(bb - P.radius);
@@ -146,14 +168,6 @@ dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__
         for (int k = 0; k < 4; ++k)
             if (t.wgt[k] != 0.f) atomicAdd(gc + t.idx[k], gv * t.wgt[k]);
     }
-}
-
-typedef __attribute__((ext_vector_type(4))) float f4_t;
-
-template <bool NT>
-__device__ __forceinline__ void st4(float* p, f4_t v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(p));
-    else *reinterpret_cast<f4_t*>(p) = v;
 }
 
 // ---- unit-step fast path ---------------------------------------------------------------------
@@ -929,7 +943,14 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
         return check_launch("rmd_dicl_stack/patch");
     }
     dim3 grid((height * width / 4 + kThreads - 1) / kThreads, d * d, batch);
-    dicl_stack_kernel<<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
+    // RMD_DICL_GENERAL (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = channel loop unrolled by 2
+    const int var = env_variant("RMD_DICL_GENERAL");
+    if (var == 1)
+        dicl_stack_kernel<false, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
+    else if (var == 2)
+        dicl_stack_kernel<true, 2><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
+    else
+        dicl_stack_kernel<true, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
     return check_launch("rmd_dicl_stack");
 }
 

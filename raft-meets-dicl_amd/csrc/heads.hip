@@ -96,12 +96,15 @@ __global__ void __launch_bounds__(kThreads) up8_kernel(const float* __restrict__
     }
     const size_t W8 = (size_t)8 * w;
     const size_t row = (size_t)(8 * y + i) * W8 + 8 * x;
-    float4* o0 = reinterpret_cast<float4*>(out + ((size_t)b * 2 + 0) * 64 * n + row);
-    float4* o1 = reinterpret_cast<float4*>(out + ((size_t)b * 2 + 1) * 64 * n + row);
-    o0[0] = make_float4(r0[0], r0[1], r0[2], r0[3]);
-    o0[1] = make_float4(r0[4], r0[5], r0[6], r0[7]);
-    o1[0] = make_float4(r1[0], r1[1], r1[2], r1[3]);
-    o1[1] = make_float4(r1[4], r1[5], r1[6], r1[7]);
+    // the upsampled flow is written once per iteration: non-temporal stores keep it out of the way
+    // of the mask/flow lines neighbouring lanes re-read
+    typedef __attribute__((ext_vector_type(4))) float v4;
+    v4* o0 = reinterpret_cast<v4*>(out + ((size_t)b * 2 + 0) * 64 * n + row);
+    v4* o1 = reinterpret_cast<v4*>(out + ((size_t)b * 2 + 1) * 64 * n + row);
+    __builtin_nontemporal_store(v4{r0[0], r0[1], r0[2], r0[3]}, o0);
+    __builtin_nontemporal_store(v4{r0[4], r0[5], r0[6], r0[7]}, o0 + 1);
+    __builtin_nontemporal_store(v4{r1[0], r1[1], r1[2], r1[3]}, o1);
+    __builtin_nontemporal_store(v4{r1[4], r1[5], r1[6], r1[7]}, o1 + 1);
 }
 
 // Backward, pass 1.  Block (64 pixels, 8 sub-rows), grid (ceil(N/64), B).  Writes d mask and the

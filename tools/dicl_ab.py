@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the DICL volume kernel variants (RMD_DICL_PATCH / RMD_DICL_INT, read per launch) at the
-BASELINE shapes: a6 rmd_dicl_stack at cfg4 1/8 (B8 C32 48x160 r4), a8 rmd_dicl_stack_int at cfg3
+"""A/B of the DICL volume kernel variants (RMD_DICL_PATCH / RMD_DICL_GENERAL / RMD_DICL_INT, read per launch) at the
+BASELINE shapes: a6 rmd_dicl_stack at cfg4 1/8 (B8 C32 48x160 r4), a7 its raft_dicl_ml level-1 form (f2 at 24x80), a8 rmd_dicl_stack_int at cfg3
 level 2 (B8 C32 96x128 ru=rv=3).  Each variant's output is compared bitwise with variant 1's (the
 previous formulation); times are medians of HIP-event-timed launches, interleaved over rounds.
 usage: python tools/dicl_ab.py [reps] -> one JSON document on stdout"""
@@ -43,6 +43,9 @@ def main():
     nb = b * 81 * 2 * c * h * w * 4 + 2 * f1.numel() * 4 + co.numel() * 4
     out = torch.empty(b, 9, 9, 2 * c, h, w, device=dev)
     cases.append(("a6_stack_cfg4", "RMD_DICL_PATCH", ["1", "0", "2", "3"], lambda: ops.dicl_stack(f1, f2, co, r), nb))
+    f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
+    cases.append(("a7_ml_level1_cfg4", "RMD_DICL_GENERAL", ["1", "0", "2"],
+                  lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), nb - f2.numel() * 3))
     b3, c3, h3, w3 = 8, 32, 96, 128
     g1 = torch.randn(b3, c3, h3, w3, generator=g).to(dev)
     g2 = torch.randn(b3, c3, h3, w3, generator=g).to(dev)
