@@ -284,13 +284,14 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
 // patch row; rows past the window go straight to global float atomics; the window is then added
 // to grad_f2 once per element.  grid (pixels/256, C, B).
 constexpr int kWinFloats = 12288;      // 48 KiB LDS window
+constexpr int kWinSmall = 4096;        // 16 KiB LDS window (narrow maps, see rmd_dicl_stack_backward)
 
-template <int R>
+template <int R, int WIN, int ABL = 0>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                  float* __restrict__ gf1, float* __restrict__ gf2) {
     constexpr int D = 2 * R + 1, K = 2 * R + 2;
-    __shared__ float win[kWinFloats];
+    __shared__ float win[WIN];
     __shared__ int wmin;
     const int n = P.h * P.w, nl = P.hl * P.wl;
     const int p = blockIdx.x * kThreads + threadIdx.x;
@@ -310,12 +311,12 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
         ys = (int)fy0 - R;
     }
     if (threadIdx.x == 0) wmin = 1 << 30;
-    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
     __syncthreads();
     if (pv) atomicMin(&wmin, max(ys, 0));
     __syncthreads();
     const int wy0 = min(wmin, P.hl);
-    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
     const int C = P.C, C2 = 2 * C + P.extra;
     const size_t dstride = (size_t)C2 * n;
     float* g2c = gf2 + ((size_t)b * C + c) * nl;
@@ -333,8 +334,12 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
                     const float* gd = gp + (size_t)(a * D + j) * dstride;
-                    s1 += gd[(size_t)c * n];
-                    gr[a] = gd[(size_t)(C + c) * n];
+                    if constexpr (ABL == 3) {
+                        gr[a] = fx * (float)(a + j);
+                    } else {
+                        s1 += gd[(size_t)c * n];
+                        gr[a] = gd[(size_t)(C + c) * n];
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i)
@@ -345,12 +350,25 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
             }
             const int yy = ys + j;
             if (yy >= 0 && yy < P.hl) {
-                const bool in_win = yy - wy0 < wrows;
-                float* r = in_win ? win + (size_t)(yy - wy0) * P.wl : g2c + (size_t)yy * P.wl;
+                // LDS and global targets in separate branches: a pointer selected between them is
+                // generic, and flat atomics into LDS cost 4x the whole kernel (0.96 vs 0.23 ms)
+                if (yy - wy0 < wrows) {
+                    float* r = win + (yy - wy0) * P.wl;
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const int xx = xs + i;
-                    if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xs + i;
+                        if (ABL == 4) {      // diagnostic: same adds, consecutive ones on disjoint rows
+                            if (xx >= 0 && xx < P.wl) atomicAdd(win + ((j + i) % 24) * P.wl + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
+                        } else if (ABL != 2 && xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
+                        if (ABL == 2) s1 += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                    }
+                } else {
+                    float* r = g2c + (size_t)yy * P.wl;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xs + i;
+                        if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
+                    }
                 }
             }
 #pragma unroll
@@ -362,7 +380,7 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
     float* gw = g2c + (size_t)wy0 * P.wl;
     for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
         const float v = win[k];
-        if (v != 0.f) atomicAdd(gw + k, v);
+        if (ABL != 1 && v != 0.f) atomicAdd(gw + k, v);
     }
 }
 
@@ -371,10 +389,11 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
 // f1-half gradients into grad_f1 (plain store) and its 4 f2 taps into the workgroup's LDS window
 // (rows [wy0, wy0 + wrows) from the group's lowest tap row; taps past it go to global atomics);
 // the window is then added to grad_f2 once per element.  grid (pixels/256, C, B).
+template <int WIN>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                    float* __restrict__ gf1, float* __restrict__ gf2) {
-    __shared__ float win[kWinFloats];
+    __shared__ float win[WIN];
     __shared__ int wmin;
     const int n = P.h * P.w, nl = P.hl * P.wl;
     const int p = blockIdx.x * kThreads + threadIdx.x;
@@ -387,7 +406,7 @@ dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __r
         cys = coords[(size_t)b * 2 * n + n + p] * P.inv_scale;
     }
     if (threadIdx.x == 0) wmin = 1 << 30;
-    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
     __syncthreads();
     if (pv) {
         // lowest tap row of this pixel: y of displacement bb = 0 (sy >= 0), clamped into the level
@@ -396,7 +415,7 @@ dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __r
     }
     __syncthreads();
     const int wy0 = min(wmin, P.hl);
-    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
     const int C = P.C, C2 = 2 * C + P.extra;
     const size_t dstride = (size_t)C2 * n;
     float* g2c = gf2 + ((size_t)b * C + c) * nl;
@@ -415,8 +434,8 @@ dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __r
                 for (int k = 0; k < 4; ++k) {
                     if (t.wgt[k] == 0.f) continue;
                     const int yy = t.idx[k] / P.wl;
-                    float* dst = (yy >= wy0 && yy - wy0 < wrows) ? win + (t.idx[k] - wy0 * P.wl) : g2c + t.idx[k];
-                    atomicAdd(dst, gv * t.wgt[k]);
+                    if (yy >= wy0 && yy - wy0 < wrows) atomicAdd(win + (t.idx[k] - wy0 * P.wl), gv * t.wgt[k]);
+                    else atomicAdd(g2c + t.idx[k], gv * t.wgt[k]);
                 }
             }
         }
@@ -436,11 +455,11 @@ dicl_stack_general_backward_kernel(const float* __restrict__ g, const float* __r
 // K FMAs per displacement plus K^2 per row bb, all in registers, then K^2 window atomics per lane
 // instead of 4 per displacement (324 for r = 4).  A lane whose taps do not fit the patch (fp32
 // rounding at an exact span bound) takes the per-tap path, so the result never depends on K.
-template <int K>
+template <int K, int WIN>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                float* __restrict__ gf1, float* __restrict__ gf2) {
-    __shared__ float win[kWinFloats];
+    __shared__ float win[WIN];
     __shared__ int wmin;
     const int n = P.h * P.w, nl = P.hl * P.wl;
     const int p = blockIdx.x * kThreads + threadIdx.x;
@@ -453,14 +472,14 @@ dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restr
         cys = fminf(fmaxf(coords[(size_t)b * 2 * n + n + p] * P.inv_scale, -1.0e6f), 1.0e6f);
     }
     if (threadIdx.x == 0) wmin = 1 << 30;
-    for (int k = threadIdx.x; k < kWinFloats; k += kThreads) win[k] = 0.f;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
     __syncthreads();
     const float py0 = (cys - (float)P.radius) * P.sy, px0 = (cxs - (float)P.radius) * P.sx;
     const int ybase = (int)floorf(py0), xbase = (int)floorf(px0);
     if (pv) atomicMin(&wmin, min(max(ybase, 0), P.hl));
     __syncthreads();
     const int wy0 = min(wmin, P.hl);
-    const int wrows = min(P.hl - wy0, kWinFloats / P.wl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
     const int C = P.C, C2 = 2 * C + P.extra;
     const size_t dstride = (size_t)C2 * n;
     float* g2c = gf2 + ((size_t)b * C + c) * nl;
@@ -506,12 +525,20 @@ dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restr
             for (int j = 0; j < K; ++j) {
                 const int yy = ybase + j;
                 if (yy < 0 || yy >= P.hl) continue;
-                const bool in_win = yy >= wy0 && yy - wy0 < wrows;
-                float* r = in_win ? win + (size_t)(yy - wy0) * P.wl : g2c + (size_t)yy * P.wl;
+                if (yy >= wy0 && yy - wy0 < wrows) {        // LDS / global in separate branches (no flat atomics)
+                    float* r = win + (yy - wy0) * P.wl;
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const int xx = xbase + i;
-                    if (xx >= 0 && xx < P.wl && patch[j][i] != 0.f) atomicAdd(r + xx, patch[j][i]);
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xbase + i;
+                        if (xx >= 0 && xx < P.wl && patch[j][i] != 0.f) atomicAdd(r + xx, patch[j][i]);
+                    }
+                } else {
+                    float* r = g2c + (size_t)yy * P.wl;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xbase + i;
+                        if (xx >= 0 && xx < P.wl && patch[j][i] != 0.f) atomicAdd(r + xx, patch[j][i]);
+                    }
                 }
             }
         } else {
@@ -526,8 +553,8 @@ dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restr
                     for (int k = 0; k < 4; ++k) {
                         if (t.wgt[k] == 0.f) continue;
                         const int yy = t.idx[k] / P.wl;
-                        float* dst = (yy >= wy0 && yy - wy0 < wrows) ? win + (t.idx[k] - wy0 * P.wl) : g2c + t.idx[k];
-                        atomicAdd(dst, gv * t.wgt[k]);
+                        if (yy >= wy0 && yy - wy0 < wrows) atomicAdd(win + (t.idx[k] - wy0 * P.wl), gv * t.wgt[k]);
+                        else atomicAdd(g2c + t.idx[k], gv * t.wgt[k]);
                     }
                 }
             }
@@ -965,11 +992,28 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
     const int d = 2 * radius + 1;
+    // LDS window: a workgroup's 256 pixels cover ~256/w + 1 rows; with the patch (<= 2r+2 rows at
+    // unit steps) and some flow spread, 4096 floats (16 KiB) hold them for w up to ~170 and leave
+    // room for 9 workgroups per CU instead of 3 (48 KiB); rows past the window still go to global
+    // atomics, so the choice only affects speed.  RMD_DICL_BWD_WIN=1 forces the 48 KiB window (A/B).
+    const float rows_est = 2.0f * radius * std::max(P.sy, 1.0f) + 256.0f / width * std::max(P.sy, 0.5f) + 10.0f;
+    const bool small_win = rows_est * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
     if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
         (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        const int abl = env_variant("RMD_DICL_BWD_ABL");     // diagnostic ablation (results wrong)
+        if (radius == 4 && abl >= 1 && abl <= 4 && P.wl * 24 <= kWinSmall) {
+            if (abl == 1) dicl_stack_patch_backward_kernel<4, kWinSmall, 1><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+            if (abl == 2) dicl_stack_patch_backward_kernel<4, kWinSmall, 2><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+            if (abl == 3) dicl_stack_patch_backward_kernel<4, kWinSmall, 3><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+            if (abl == 4) dicl_stack_patch_backward_kernel<4, kWinSmall, 4><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+            return check_launch("rmd_dicl_stack_backward/patch-ablation");
+        }
         switch (radius) {
-#define RMD_CASE(RR) case RR: dicl_stack_patch_backward_kernel<RR><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); break;
+#define RMD_CASE(RR) case RR: \
+            if (small_win) dicl_stack_patch_backward_kernel<RR, kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+            else dicl_stack_patch_backward_kernel<RR, kWinFloats><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+            break;
             RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE
         }
@@ -983,7 +1027,10 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
         const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
         switch (k) {
-#define RMD_KCASE(KK) case KK: dicl_stack_sep_backward_kernel<KK><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); return check_launch("rmd_dicl_stack_backward/separable");
+#define RMD_KCASE(KK) case KK: \
+            if (small_win) dicl_stack_sep_backward_kernel<KK, kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+            else dicl_stack_sep_backward_kernel<KK, kWinFloats><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+            return check_launch("rmd_dicl_stack_backward/separable");
             RMD_KCASE(4) RMD_KCASE(6) RMD_KCASE(8) RMD_KCASE(10)
 #undef RMD_KCASE
             default: break;
@@ -991,7 +1038,8 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
     }
     if (level_width <= kWinFloats && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sy >= 0.f) {
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
-        dicl_stack_general_backward_kernel<<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+        if (small_win) dicl_stack_general_backward_kernel<kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
+        else dicl_stack_general_backward_kernel<kWinFloats><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
         return check_launch("rmd_dicl_stack_backward/general");
     }
     dim3 g1((height * width / 4 + kThreads - 1) / kThreads, channels, batch);

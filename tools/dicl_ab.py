@@ -53,6 +53,35 @@ def main():
     nb3 = b3 * 49 * 2 * c3 * h3 * w3 * 4 + 2 * g1.numel() * 4
     cases.append(("a8_int_cfg3", "RMD_DICL_INT", ["1", "0", "2", "3"], lambda: ops.dicl_stack_int(g1, g2, 3, 3), nb3))
     del out
+    # backward (training): forward+backward minus forward; window variants (atomics: compare allclose)
+    f1g, f2g, f2lg = (t.clone().requires_grad_(True) for t in (f1, f2, f2l))
+    gst = torch.randn(b, 9, 9, 2 * c, h, w, generator=g).to(dev)
+
+    def bwd6():
+        return torch.autograd.grad(ops.dicl_stack(f1g, f2g, co, r), (f1g, f2g), gst)
+
+    def bwd7():
+        return torch.autograd.grad(ops.dicl_stack(f1g, f2lg, co, r, level=1, norm_hw=(h, w)), (f1g, f2lg), gst)
+    for name, fn in (("a6_backward_cfg4", bwd6), ("a7_backward_cfg4", bwd7)):
+        out = {}
+        os.environ["RMD_DICL_BWD_WIN"] = "1"
+        ref = [t.clone() for t in fn()]
+        tt = {"1": [], "0": []}
+        for _ in range(3):
+            for v in ("1", "0"):
+                os.environ["RMD_DICL_BWD_WIN"] = v
+                fn()
+                tt[v].append(med_ms(fn, reps))
+        for v in ("1", "0"):
+            os.environ["RMD_DICL_BWD_WIN"] = v
+            got = fn()
+            err = max(float((a - b_).abs().max() / b_.abs().max()) for a, b_ in zip(got, ref))
+            out[v] = dict(fwd_bwd_ms=min(tt[v]), all_ms=tt[v], max_rel_err_vs_v1=err)
+        os.environ.pop("RMD_DICL_BWD_WIN", None)
+        res[name] = out
+        del ref
+    del gst, f1g, f2g, f2lg
+    torch.cuda.empty_cache()
     for name, env, variants, fn, nbytes in cases:
         os.environ[env] = "1"
         ref = fn().clone()
