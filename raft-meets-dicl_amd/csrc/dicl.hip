@@ -384,6 +384,163 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
     }
 }
 
+// Same backward with 4 consecutive pixels per lane.  LDS float atomics are the cost of the one-pixel
+// kernel (0.98 ms at cfg4, 0.23 ms with them dropped: ~100 cycles per ds_add_f32 wave-instruction),
+// so a lane first merges its pixels' patch rows in registers: when the 4 patches share a top row
+// and start at consecutive columns (smooth flow: the common case) row j of the 4 patches is one
+// (2r+5)-wide run, 13 adds instead of 40 at r = 4.  Otherwise every pixel adds its own row.  The
+// gradient rows are read as float4 (1 KiB per wave-instruction).  grid (pixels/1024, C, B).
+template <int R, int WIN, int PX>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                                  float* __restrict__ gf1, float* __restrict__ gf2) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, M = K + PX - 1;
+    __shared__ float win[WIN];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * PX;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p0 < n;               // n % 4 == 0: a lane's PX pixels are all valid or all not
+    float fx[PX], fy[PX];
+    int xs[PX], ys[PX];
+    int ymin = 1 << 30;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        fx[k] = fy[k] = 0.f;
+        xs[k] = 0;
+        ys[k] = 1 << 30;
+        if (pv) {
+            float cx = coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale;
+            float cy = coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale;
+            cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+            cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+            const float fx0 = floorf(cx), fy0 = floorf(cy);
+            fx[k] = cx - fx0;
+            fy[k] = cy - fy0;
+            xs[k] = (int)fx0 - R;
+            ys[k] = (int)fy0 - R;
+            ymin = min(ymin, max(ys[k], 0));
+        }
+    }
+    bool merged = true;
+#pragma unroll
+    for (int k = 1; k < PX; ++k) merged = merged && ys[k] == ys[0] && xs[k] == xs[0] + k;
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    if (pv) atomicMin(&wmin, ymin);
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    typedef typename FVec<PX>::T v4;
+    if (pv) {
+        // wave-uniform plane base + 32-bit lane offsets (saddr + voffset; the host keeps a batch
+        // image's gradient volume below 4 GiB)
+        const char* gb = reinterpret_cast<const char*>(g + (size_t)b * D * D * dstride);
+        const unsigned lo1 = (unsigned)(((size_t)c * n + p0) * sizeof(float));
+        const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
+        v4 s1 = v4(0.f);
+        float qprev[PX][K];
+#pragma unroll
+        for (int k = 0; k < PX; ++k)
+#pragma unroll
+            for (int i = 0; i < K; ++i) qprev[k][i] = 0.f;
+#pragma unroll 1
+        for (int j = 0; j < K; ++j) {      // rolled: unrolled, the scheduler hoists later rows' loads (256 VGPRs)
+            float qcur[PX][K];
+            if (j < D) {
+                v4 gr[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const char* gd = gb + (size_t)(a * D + j) * dstride * sizeof(float);
+                    s1 += *reinterpret_cast<const v4*>(gd + lo1);
+                    gr[a] = *reinterpret_cast<const v4*>(gd + lo2);
+                }
+#pragma unroll
+                for (int k = 0; k < PX; ++k)
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        qcur[k][i] = (i < D ? gr[i][k] * (1.0f - fx[k]) : 0.f) + (i >= 1 ? gr[i - 1][k] * fx[k] : 0.f);
+            } else {
+#pragma unroll
+                for (int k = 0; k < PX; ++k)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) qcur[k][i] = 0.f;
+            }
+            // row j of the patches, computed in place of the previous row's x-spread
+            float (&val)[PX][K] = qprev;
+#pragma unroll
+            for (int k = 0; k < PX; ++k)
+#pragma unroll
+                for (int i = 0; i < K; ++i) val[k][i] = qcur[k][i] * (1.0f - fy[k]) + qprev[k][i] * fy[k];
+            if (merged) {
+                const int yy = ys[0] + j;
+                if (yy >= 0 && yy < P.hl) {
+                    float m[M];
+#pragma unroll
+                    for (int t = 0; t < M; ++t) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int k = 0; k < PX; ++k)
+                            if (t - k >= 0 && t - k < K) acc += val[k][t - k];
+                        m[t] = acc;
+                    }
+                    if (yy - wy0 < wrows) {      // LDS / global in separate branches (no flat atomics)
+                        float* r = win + (yy - wy0) * P.wl;
+#pragma unroll
+                        for (int t = 0; t < M; ++t) {
+                            const int xx = xs[0] + t;
+                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, m[t]);
+                        }
+                    } else {
+                        float* r = g2c + (size_t)yy * P.wl;
+#pragma unroll
+                        for (int t = 0; t < M; ++t) {
+                            const int xx = xs[0] + t;
+                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, m[t]);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < PX; ++k) {
+                    const int yy = ys[k] + j;
+                    if (yy < 0 || yy >= P.hl) continue;
+                    if (yy - wy0 < wrows) {
+                        float* r = win + (yy - wy0) * P.wl;
+#pragma unroll
+                        for (int i = 0; i < K; ++i) {
+                            const int xx = xs[k] + i;
+                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, val[k][i]);
+                        }
+                    } else {
+                        float* r = g2c + (size_t)yy * P.wl;
+#pragma unroll
+                        for (int i = 0; i < K; ++i) {
+                            const int xx = xs[k] + i;
+                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, val[k][i]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < PX; ++k)
+#pragma unroll
+                for (int i = 0; i < K; ++i) qprev[k][i] = qcur[k][i];
+        }
+        *reinterpret_cast<v4*>(gf1 + ((size_t)b * C + c) * n + p0) = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
+    }
+}
+
 // backward of the general (scaled-grid) stack, raft_dicl_ml levels > 0: every displacement has its
 // own bilinear weights, so each lane (pixel p, channel c) walks the (2r+1)^2 displacements, adds its
 // f1-half gradients into grad_f1 (plain store) and its 4 f2 taps into the workgroup's LDS window
@@ -998,9 +1155,28 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
     // atomics, so the choice only affects speed.  RMD_DICL_BWD_WIN=1 forces the 48 KiB window (A/B).
     const float rows_est = 2.0f * radius * std::max(P.sy, 1.0f) + 256.0f / width * std::max(P.sy, 0.5f) + 10.0f;
     const bool small_win = rows_est * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
+    const double image_bytes = 4.0 * d * d * (2.0 * channels + P.extra) * height * width;
     if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
         (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        // 4 pixels per lane with merged patch rows (default), RMD_DICL_BWD_PX=1: one pixel per lane
+        if (env_variant("RMD_DICL_BWD_PX") != 1 && env_variant("RMD_DICL_BWD_ABL") == 0 && image_bytes < 4294967296.0) {
+            const int px = env_variant("RMD_DICL_BWD_PX") == 4 ? 4 : 2;     // 4: A/B (256 VGPRs at r = 4)
+            const float rows4 = 2.0f * radius + 256.0f * px / width + 10.0f;
+            const bool small4 = rows4 * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
+            dim3 grid4((height * width / px + kThreads - 1) / kThreads, channels, batch);
+            switch (radius) {
+#define RMD_CASE(RR) case RR: \
+                if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                break;
+                RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
+#undef RMD_CASE
+            }
+            return check_launch("rmd_dicl_stack_backward/patch4");
+        }
         const int abl = env_variant("RMD_DICL_BWD_ABL");     // diagnostic ablation (results wrong)
         if (radius == 4 && abl >= 1 && abl <= 4 && P.wl * 24 <= kWinSmall) {
             if (abl == 1) dicl_stack_patch_backward_kernel<4, kWinSmall, 1><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
