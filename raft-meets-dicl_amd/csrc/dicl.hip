@@ -123,6 +123,115 @@ dicl_stack_kernel(const float* __restrict__ f1, const float* __restrict__ f2, co
     }
 }
 
+// Scaled-grid forward (raft_dicl_ml levels > 0, sx, sy < 1): displacement (a, bb) samples
+// x = (cx + a - r) sx, y = (cy + bb - r) sy, so all (2r+1)^2 samples of a pixel lie in a K x K
+// integer patch (K = floor(2 r s) + 2, rounded up to even) and the x weights depend on a only, the
+// y weights on bb only.  One lane per (pixel, channel) loads the patch once (K^2 loads instead of
+// 4 (2r+1)^2 gathers), interpolates along x into K row values per a, then along y with per-bb
+// weight vectors held in registers; lanes whose samples leave the patch (fp32 rounding at an
+// exact span bound) fall back to the per-tap formula.  Stores: wave-uniform plane base + 32-bit
+// lane offset, non-temporal.  grid (pixels/256, C, B).
+template <int R, int K, bool NT>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_sep_kernel(const float* __restrict__ f1, const float* __restrict__ f2, const float* __restrict__ coords,
+                      StackParams P, float* __restrict__ out) {
+    constexpr int D = 2 * R + 1;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int c = blockIdx.y, b = blockIdx.z;
+    if (p >= n) return;
+    const float cxs = fminf(fmaxf(coords[(size_t)b * 2 * n + p] * P.inv_scale, -1.0e6f), 1.0e6f);
+    const float cys = fminf(fmaxf(coords[(size_t)b * 2 * n + n + p] * P.inv_scale, -1.0e6f), 1.0e6f);
+    const int xbase = (int)floorf((cxs - (float)R) * P.sx), ybase = (int)floorf((cys - (float)R) * P.sy);
+    int rx[D], ry[D];
+    float fxa[D], fyb[D];
+    bool fits = true;
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const float px = fminf(fmaxf((cxs + (float)(a - R)) * P.sx, -1.0e6f), 1.0e6f);
+        const float py = fminf(fmaxf((cys + (float)(a - R)) * P.sy, -1.0e6f), 1.0e6f);
+        const float x0 = floorf(px), y0 = floorf(py);
+        rx[a] = (int)x0 - xbase;
+        ry[a] = (int)y0 - ybase;
+        fxa[a] = px - x0;
+        fyb[a] = py - y0;
+        fits = fits && rx[a] >= 0 && rx[a] <= K - 2 && ry[a] >= 0 && ry[a] <= K - 2;
+    }
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* const ob = out + (size_t)b * D * D * dstride;
+    const unsigned lo1 = (unsigned)(((size_t)c * n + p) * sizeof(float));
+    const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
+    const float v1 = f1[((size_t)b * C + c) * n + p];
+    const float* f2c = f2 + ((size_t)b * C + c) * nl;
+    auto put = [&](int a, int bb, float v) {
+        char* od = reinterpret_cast<char*>(ob + (size_t)(a * D + bb) * dstride);
+        if constexpr (NT) {
+            __builtin_nontemporal_store(v1, reinterpret_cast<float*>(od + lo1));
+            __builtin_nontemporal_store(v, reinterpret_cast<float*>(od + lo2));
+        } else {
+            *reinterpret_cast<float*>(od + lo1) = v1;
+            *reinterpret_cast<float*>(od + lo2) = v;
+        }
+    };
+    if (fits) {
+        float patch[K][K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int yy = ybase + j;
+            const bool rok = yy >= 0 && yy < P.hl;
+            const int roff = min(max(yy, 0), P.hl - 1) * P.wl;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int xx = xbase + i;
+                const float e = f2c[roff + min(max(xx, 0), P.wl - 1)];
+                patch[j][i] = (rok && xx >= 0 && xx < P.wl) ? e : 0.f;
+            }
+        }
+        float wy[D][K];                 // y weights of displacement row bb over the patch rows
+#pragma unroll
+        for (int bb = 0; bb < D; ++bb)
+#pragma unroll
+            for (int j = 0; j < K; ++j) wy[bb][j] = j == ry[bb] ? 1.f - fyb[bb] : (j == ry[bb] + 1 ? fyb[bb] : 0.f);
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            float col[K];               // the patch interpolated along x at displacement a, per row
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const float wx = i == rx[a] ? 1.f - fxa[a] : (i == rx[a] + 1 ? fxa[a] : 0.f);
+                    acc = fmaf(wx, patch[j][i], acc);
+                }
+                col[j] = acc;
+            }
+#pragma unroll
+            for (int bb = 0; bb < D; ++bb) {
+                float v = 0.f;
+#pragma unroll
+                for (int j = 0; j < K; ++j) v = fmaf(wy[bb][j], col[j], v);
+                put(a, bb, v);
+            }
+        }
+    } else {
+        for (int a = 0; a < D; ++a)
+            for (int bb = 0; bb < D; ++bb) {
+                const Taps t = make_taps((cxs + (float)(a - R)) * P.sx, (cys + (float)(bb - R)) * P.sy, P.hl, P.wl);
+                put(a, bb, t.wgt[0] * f2c[t.idx[0]] + t.wgt[1] * f2c[t.idx[1]] + t.wgt[2] * f2c[t.idx[2]] +
+                               t.wgt[3] * f2c[t.idx[3]]);
+            }
+    }
+    if (P.extra && c == 0) {       // dicl_emb.py:81-85: delta (dx = a-r, dy = bb-r) as two constant channels
+        for (int a = 0; a < D; ++a)
+            for (int bb = 0; bb < D; ++bb) {
+                float* od = ob + (size_t)(a * D + bb) * dstride + p;
+                od[(size_t)(2 * C) * n] = (float)(a - R);
+                od[(size_t)(2 * C + 1) * n] = (float)(bb - R);
+            }
+    }
+}
+
 // backward: grad_f1 = sum over displacements of the f1 half (deterministic, no atomics)
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_grad_f1_kernel(const float* __restrict__ g, StackParams P, float* __restrict__ gf1) {
@@ -1127,8 +1236,24 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
         return check_launch("rmd_dicl_stack/patch");
     }
     dim3 grid((height * width / 4 + kThreads - 1) / kThreads, d * d, batch);
-    // RMD_DICL_GENERAL (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = channel loop unrolled by 2
+    // RMD_DICL_GENERAL (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = channel loop unrolled by 2,
+    // 3 = per-tap kernel instead of the separable one
     const int var = env_variant("RMD_DICL_GENERAL");
+    if (var == 0 && (radius == 3 || radius == 4) && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sx >= 0.f &&
+        P.sy >= 0.f && P.sx <= 1.f && P.sy <= 1.f && image_bytes < 4294967296.0) {
+        const float span = 2.0f * radius * std::max(P.sx, P.sy);
+        const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
+        dim3 g1((height * width + kThreads - 1) / kThreads, channels, batch);
+        hipStream_t st = as_stream(stream);
+        bool launched = true;
+        switch (radius * 100 + k) {
+#define RMD_SCASE(RR, KK) case RR * 100 + KK: dicl_stack_sep_kernel<RR, KK, true><<<g1, kThreads, 0, st>>>(fmap1, fmap2, coords, P, out); break;
+            RMD_SCASE(3, 4) RMD_SCASE(3, 6) RMD_SCASE(3, 8) RMD_SCASE(4, 4) RMD_SCASE(4, 6) RMD_SCASE(4, 8)
+#undef RMD_SCASE
+            default: launched = false;
+        }
+        if (launched) return check_launch("rmd_dicl_stack/separable");
+    }
     if (var == 1)
         dicl_stack_kernel<false, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
     else if (var == 2)

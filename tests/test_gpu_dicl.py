@@ -87,6 +87,29 @@ def test_dicl_stack_cfg4_shape_vs_oracle():
     assert rel_max_err(st, ref) < 1e-5
 
 
+@pytest.mark.parametrize("level,radius,extra", [(1, 4, False), (2, 4, False), (1, 3, True), (3, 4, False)])
+def test_dicl_stack_scaled_grid_vs_oracle(level, radius, extra):
+    """raft_dicl_ml levels > 0 (grid scaled by (w_l-1)/(w-1)): the separable patch kernel (r = 3, 4;
+    K = 4, 6 at levels 1, 2) and, at level 3 (K = 4), large flows whose samples leave the map."""
+    import rmd
+    rng = np.random.default_rng(40 + level)
+    b, c, h, w = 2, 16, 24, 80
+    hl, wl = h >> level, w >> level
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, hl, wl)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    co = (np.stack([xs, ys])[None] + rng.normal(0, 3 if level < 3 else 30, (b, 2, h, w))).astype(np.float32)
+    st = rmd.ops.dicl_stack(_t(f1), _t(f2), _t(co), radius, level=level, norm_hw=(h, w), extra_delta=extra)
+    st = st.cpu().numpy()
+    ref = oracle.dicl_stack(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64), radius,
+                            level=level, norm_hw=(h, w))
+    assert rel_max_err(st[:, :, :, :2 * c], ref) < 1e-5
+    if extra:
+        a = (np.arange(2 * radius + 1) - radius).astype(np.float32)
+        assert np.array_equal(st[0, :, :, 2 * c, 3, 5], np.broadcast_to(a[:, None], st.shape[1:3]))
+        assert np.array_equal(st[0, :, :, 2 * c + 1, 3, 5], np.broadcast_to(a[None, :], st.shape[1:3]))
+
+
 def test_dicl_stack_int_golden_bit_exact():
     import rmd
     g = load_golden("dicl_cost_b2_c16_10x12")

@@ -44,7 +44,7 @@ def main():
     out = torch.empty(b, 9, 9, 2 * c, h, w, device=dev)
     cases.append(("a6_stack_cfg4", "RMD_DICL_PATCH", ["1", "0", "2", "3"], lambda: ops.dicl_stack(f1, f2, co, r), nb))
     f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
-    cases.append(("a7_ml_level1_cfg4", "RMD_DICL_GENERAL", ["1", "0", "2"],
+    cases.append(("a7_ml_level1_cfg4", "RMD_DICL_GENERAL", ["1", "3", "0"],
                   lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), nb - f2.numel() * 3))
     b3, c3, h3, w3 = 8, 32, 96, 128
     g1 = torch.randn(b3, c3, h3, w3, generator=g).to(dev)
@@ -91,7 +91,7 @@ def main():
             os.environ[env] = v
             o = fn()
             torch.cuda.synchronize()
-            same[v] = bool(torch.equal(o, ref))
+            same[v] = bool(torch.equal(o, ref)) or float((o - ref).abs().max() / ref.abs().max())
             del o
         for _ in range(3):
             for v in variants:
@@ -101,7 +101,7 @@ def main():
                 times[v].append(med_ms(fn, reps))
         os.environ.pop(env, None)
         res[name] = {v: dict(ms=min(times[v]), all_ms=times[v], GBps=nbytes / (min(times[v]) * 1e-3) / 1e9,
-                             frac_of_8TBps=nbytes / (min(times[v]) * 1e-3) / 8e12, bitwise_equal_v1=same[v])
+                             frac_of_8TBps=nbytes / (min(times[v]) * 1e-3) / 8e12, bitwise_equal_v1_or_max_rel_err=same[v])
                      for v in variants}
         del ref
         torch.cuda.empty_cache()
