@@ -278,6 +278,35 @@ int rmd_softargmax(const float* cost, int batch, int cost_channels, int pixels, 
 int rmd_softargmax_backward(const float* cost, const float* grad_flows, int batch, int cost_channels, int pixels,
                             int levels, int radius, float temperature, float* grad_cost, void* stream);
 
+/*
+ * Input format (src/models/input.py).  rmd_input_images replaces Input.__getitem__'s clip and range
+ * map (input.py:215-221), ModuloPadding.apply (input.py:79-138) and TorchAdapter's permute to NCHW
+ * (input.py:280-281) for one image tensor of a pair:
+ *   out[b, k, y, x] = (range_max - range_min) * clip(img[b, sy, sx, k], clip_min, clip_max) + range_min
+ * with (sy, sx) = (y - pad_top, x - pad_left) mapped into the image by the pad mode, or the constant
+ * 0 / 1 for RMD_PAD_ZEROS / RMD_PAD_ONES outside it.  img (B, H, W, C) float32 NHWC, out (B, C, H', W').
+ * Modes: numpy 'edge' == torch 'replicate' (EDGE), numpy/torch 'reflect' (REFLECT), numpy 'symmetric',
+ * numpy 'wrap' == torch 'circular' (WRAP).  The statistic modes (maximum, mean, median, minimum) are
+ * not provided (no config uses them; every cfg pads with zeros).
+ * rmd_input_flow replaces the flow / valid side (input.py:120-122, 301-313): flow (B, H, W, 2) float32,
+ * valid (B, H, W) bytes -> flow_out (B, 2, H', W') with NaN -> 0 and values clipped to +-flow_inf,
+ * valid_out (B, H', W') bytes; padding is zero flow / invalid.
+ */
+#define RMD_PAD_ZEROS 0
+#define RMD_PAD_ONES 1
+#define RMD_PAD_EDGE 2
+#define RMD_PAD_REFLECT 3
+#define RMD_PAD_SYMMETRIC 4
+#define RMD_PAD_WRAP 5
+
+int rmd_input_images(const float* img, int batch, int height, int width, int channels, float clip_min,
+                     float clip_max, float range_min, float range_max, int padded_height, int padded_width,
+                     int pad_top, int pad_left, int mode, float* out, void* stream);
+
+int rmd_input_flow(const float* flow, const unsigned char* valid, int batch, int height, int width,
+                   int padded_height, int padded_width, int pad_top, int pad_left, float flow_inf, float* flow_out,
+                   unsigned char* valid_out, void* stream);
+
 /* Message for the last failing call on this thread ("" if none). */
 const char* rmd_last_error(void);
 

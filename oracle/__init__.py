@@ -14,8 +14,10 @@ from .corr import (corr_volume, corr_pyramid, corr_lookup, corr_lookup_fs, corr_
 from .dicl import (dicl_stack, dicl_stack_backward, dicl_stack_int, dicl_stack_int_backward, dap, dap_backward,
                    warp_backwards, warp_backwards_backward)
 from .heads import up8, up8_backward, softargmax, softargmax_backward
+from .input import input_images, input_flow, pad_extents
 
 __all__ = ["corr_volume", "corr_pyramid", "corr_lookup", "corr_lookup_fs", "corr_lookup_backward",
            "pyramid_level_shapes", "dicl_stack", "dicl_stack_backward", "dicl_stack_int",
            "dicl_stack_int_backward", "dap", "dap_backward", "up8", "up8_backward", "softargmax",
-           "softargmax_backward", "warp_backwards", "warp_backwards_backward"]
+           "softargmax_backward", "warp_backwards", "warp_backwards_backward", "input_images", "input_flow",
+           "pad_extents"]

@@ -11,9 +11,10 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.dicl.compute_cost                 <- src/models/impls/dicl.py:171-241 (+ fused warp)
   rmd.warp.warp_backwards               <- src/models/common/warp.py:5-33
   rmd.raft.Up8Network / SoftArgMax*     <- src/models/impls/raft.py:98-190,299-331 (rmd.heads)
+  rmd.input.InputSpec / ModuloPadding   <- src/models/input.py:32-313 (frame pair + flow target format)
 """
 
-from . import blocks, corr, dicl, heads, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
+from . import blocks, corr, dicl, heads, input, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

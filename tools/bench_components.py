@@ -14,6 +14,8 @@ The MatchingNet that consumes a6/a8 (MIOpen convolutions, out of scope) is timed
   * f1  on-the-fly lookup (rmd_corr_otf_*) at cfg2: prepare + per-lookup time, bf16 / fp32
   * f2  flow heads at cfg2 (B=8, 55x128): rmd_up8 (+backward), rmd_softargmax L=4 r=4 (+backward),
         each beside the reference's eager torch formulation on the same GPU (raft.py:112-135, 319-331)
+  * f4  input format (rmd.input: clip + range + modulo padding + NCHW) for 8 frame pairs at 436x1024,
+        beside the reference's numpy path plus the host-to-device copy
   * f3  warped DICL volume (rmd_dicl_stack_int_warped) at cfg3 level 2 (B=8, C=32, 96x128, ru=rv=3) and
         rmd_warp_backwards alone, beside the reference's eager warp (warp.py:5-33)
 usage: python tools/bench_components.py [reps] [fs|heads]   -> one JSON document on stdout
@@ -257,6 +259,27 @@ def heads(res, reps, dev, g):
     res["f2_softargmax_backward_L4_r4_cfg2"] = entry(
         timed(lambda: torch.autograd.grad(fl, cg, gfl, retain_graph=True), reps),
         (2 * cost.numel() + L * b * 2 * n) * 4)
+
+    # f4: input format at cfg2 (8 frame pairs 436x1024 RGB -> padded 440x1024 NCHW in [-1, 1]), frames
+    # already resident in HBM; beside the reference's host path (numpy clip/range/pad + permute +
+    # host-to-device copy of the padded pair), input.py:208-281
+    import numpy as np
+    from rmd.input import InputSpec, ModuloPadding
+    spec = InputSpec(padding=ModuloPadding("zeros", [8, 8]))
+    fr = torch.rand(b, 436, 1024, 3, generator=g)
+    fr1, fr2 = fr.to(dev), fr.flip(0).to(dev)
+    nbytes = 2 * (fr.numel() * 4 + b * 3 * 440 * 1024 * 4)
+    npf = fr.numpy()
+
+    def host_ref():
+        out = []
+        for im in (npf, npf[::-1]):
+            x = 2.0 * np.clip(im, 0.0, 1.0) - 1.0
+            x = np.pad(x, ((0, 0), (0, 4), (0, 0), (0, 0)), mode="constant", constant_values=0.0)
+            out.append(torch.from_numpy(x).float().permute(0, 3, 1, 2).to(dev))
+        return out
+    res["f4_input_pair_cfg2"] = entry(timed(lambda: spec.prepare(fr1, fr2), reps), nbytes,
+                                      host_numpy_plus_copy_ms=timed(host_ref, max(3, reps // 4)))
 
 
 if __name__ == "__main__":
