@@ -1083,8 +1083,11 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
 #pragma unroll
         for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 512 * s);
     }
-    if (stagger && w >= 4)           // desynchronise the two waves of each SIMD (diagnostic knob)
-        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
+    // diagnostic knobs: stagger % 1000 = s_sleep(16) count that desynchronises the two waves of each
+    // SIMD; stagger >= 1000 = static s_setprio 1 for the second-dispatched half (waves 4-7)
+    if ((stagger % 1000) && w >= 4)
+        for (int i = 0; i < stagger % 1000; ++i) __builtin_amdgcn_s_sleep(16);
+    if (stagger >= 1000 && w >= 4) __builtin_amdgcn_s_setprio(1);
     while (true) {
         f32x16 acc[8];
         const int qn = qt + stride;

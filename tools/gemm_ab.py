@@ -33,7 +33,8 @@ def main():
         kern, _, aux = kern.partition("@")          # e.g. "w8@2" = RMD_STORE_AUX=2
         kern, _, knobs = kern.partition("+")        # e.g. "w8+roll+stag4" = RMD_W8_ROLL=1, RMD_W8_STAGGER=4
         os.environ["RMD_W8_ROLL"] = "1" if "roll" in knobs else "0"
-        os.environ["RMD_W8_STAGGER"] = knobs.split("stag")[1].split("+")[0] if "stag" in knobs else "0"
+        stag = int(knobs.split("stag")[1].split("+")[0]) if "stag" in knobs else 0
+        os.environ["RMD_W8_STAGGER"] = str(stag + (1000 if "prio" in knobs else 0))     # "w8+prio" = s_setprio 1 on waves 4-7
         os.environ["RMD_GEMM_KERNEL"] = kern
         os.environ["RMD_ABLATE"] = abl or "0"
         os.environ["RMD_STORE_AUX"] = aux or "2"
