@@ -499,7 +499,7 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
 // and start at consecutive columns (smooth flow: the common case) row j of the 4 patches is one
 // (2r+5)-wide run, 13 adds instead of 40 at r = 4.  Otherwise every pixel adds its own row.  The
 // gradient rows are read as float4 (1 KiB per wave-instruction).  grid (pixels/1024, C, B).
-template <int R, int WIN, int PX>
+template <int R, int WIN, int PX, bool CHAIN>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                   float* __restrict__ gf1, float* __restrict__ gf2) {
@@ -534,6 +534,18 @@ dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __re
     bool merged = true;
 #pragma unroll
     for (int k = 1; k < PX; ++k) merged = merged && ys[k] == ys[0] && xs[k] == xs[0] + k;
+    merged = merged && pv;
+    // CHAIN: lane l's merged run continues lane l-1's (same patch top row, start PX columns further)
+    // -> the wave sums overlapping runs with DPP lane shifts and each lane adds only its own PX
+    // columns (a chain's last lane adds its whole tail): 2 LDS adds per row instead of 2r+2+PX-1.
+    bool link = false, link_next = false;
+    if constexpr (CHAIN) {
+        const int pys = __builtin_amdgcn_update_dpp((int)0x80000000, ys[0], 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const int pxs = __builtin_amdgcn_update_dpp((int)0x80000000, xs[0], 0x138, 0xf, 0xf, false);
+        const int pm = __builtin_amdgcn_update_dpp(0, (int)merged, 0x138, 0xf, 0xf, false);
+        link = merged && pm != 0 && pys == ys[0] && pxs + PX == xs[0];
+        link_next = __builtin_amdgcn_update_dpp(0, (int)link, 0x130, 0xf, 0xf, false) != 0;              // wave_shl:1
+    }
     if (threadIdx.x == 0) wmin = 1 << 30;
     for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
     __syncthreads();
@@ -597,19 +609,33 @@ dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __re
                             if (t - k >= 0 && t - k < K) acc += val[k][t - k];
                         m[t] = acc;
                     }
+                    if constexpr (CHAIN) {
+                        // r_t = sum over the chain's lanes l-k of m_{l-k}[t + PX k]: all at column xs_l + t
+#pragma unroll
+                        for (int t = 0; t < M; ++t) {
+                            const int kmax = (M - 1 - t) / PX;
+                            float rr = m[t + PX * kmax];
+#pragma unroll
+                            for (int k = kmax - 1; k >= 0; --k) {
+                                const float up = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rr), 0x138, 0xf, 0xf, false));
+                                rr = m[t + PX * k] + (link ? up : 0.f);
+                            }
+                            m[t] = (t < PX || !link_next) ? rr : 0.f;
+                        }
+                    }
                     if (yy - wy0 < wrows) {      // LDS / global in separate branches (no flat atomics)
                         float* r = win + (yy - wy0) * P.wl;
 #pragma unroll
                         for (int t = 0; t < M; ++t) {
                             const int xx = xs[0] + t;
-                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, m[t]);
+                            if (xx >= 0 && xx < P.wl && (!CHAIN || t < PX || !link_next)) atomicAdd(r + xx, m[t]);
                         }
                     } else {
                         float* r = g2c + (size_t)yy * P.wl;
 #pragma unroll
                         for (int t = 0; t < M; ++t) {
                             const int xx = xs[0] + t;
-                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, m[t]);
+                            if (xx >= 0 && xx < P.wl && (!CHAIN || t < PX || !link_next)) atomicAdd(r + xx, m[t]);
                         }
                     }
                 }
@@ -1290,12 +1316,15 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
             const float rows4 = 2.0f * radius + 256.0f * px / width + 10.0f;
             const bool small4 = rows4 * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
             dim3 grid4((height * width / px + kThreads - 1) / kThreads, channels, batch);
+            const bool chain = env_variant("RMD_DICL_BWD_CHAIN") != 1;     // 1: no cross-lane run merge (A/B)
             switch (radius) {
 #define RMD_CASE(RR) case RR: \
-                if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (small4 && chain) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (chain) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 break;
                 RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE

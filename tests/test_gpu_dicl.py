@@ -210,3 +210,28 @@ def test_dicl_stack_backward_vs_oracle(level, radius):
                                         level=level, norm_hw=(h, w))
     assert rel_max_err(g1.cpu().numpy(), r1) < 1e-5
     assert rel_max_err(g2.cpu().numpy(), r2) < 1e-4
+
+
+@pytest.mark.parametrize("radius", [4, 2])
+def test_dicl_stack_backward_smooth_flow_vs_oracle(radius):
+    """Unit-step backward with a smooth flow (the case the cross-lane run merge of the patch
+    backward takes: neighbouring pixels' patches start at consecutive columns), plus rows with
+    jumps, out-of-map flows and map edges that break the chains."""
+    import rmd
+    rng = np.random.default_rng(77 + radius)
+    b, c, h, w = 2, 8, 24, 160
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    flow = np.stack([np.full((h, w), 2.3), np.full((h, w), -1.6)])[None].repeat(b, 0)
+    flow[1] += 0.01 * xs[None]                                  # slowly varying: chains break now and then
+    flow[0, :, 5, 40:60] += 7.5                                 # a jump inside a row
+    flow[1, :, 20:, :] -= 30.0                                  # patches partly / fully above the map
+    co = (np.stack([xs, ys])[None] + flow).astype(np.float32)
+    t1, t2 = _t(f1, True), _t(f2, True)
+    st = rmd.ops.dicl_stack(t1, t2, _t(co), radius)
+    gst = rng.standard_normal(tuple(st.shape)).astype(np.float32)
+    g1, g2 = torch.autograd.grad(st, (t1, t2), _t(gst))
+    r1, r2 = oracle.dicl_stack_backward(f2.shape, co.astype(np.float64), radius, gst.astype(np.float64))
+    assert rel_max_err(g1.cpu().numpy(), r1) < 1e-5
+    assert rel_max_err(g2.cpu().numpy(), r2) < 1e-4

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Ablation of the unit-step DICL stack backward at cfg4 (B8 C32 48x160 r4): RMD_DICL_BWD_ABL =
-0 full (default 2-pixel merged-row kernel), px1 the 1-pixel kernel, px4 the 4-pixel merged kernel; on the 1-pixel kernel: 1 no window flush (global atomics), 2 no LDS atomics, 3 no gradient loads.  Times the
+0 full (default 2-pixel merged-row kernel with the cross-lane chain), nochain without the chain, px1 the 1-pixel kernel, px4 the 4-pixel merged kernel; on the 1-pixel kernel: 1 no window flush (global atomics), 2 no LDS atomics, 3 no gradient loads.  Times the
 backward launch alone (rmd_dicl_stack_backward through the ctypes binding), HIP events, median.
 Diagnostic only (ablated results are wrong).  usage: python tools/dicl_bwd_ablate.py [reps]"""
 import json
@@ -31,8 +31,9 @@ def main():
         _lib.check(_lib.lib().rmd_dicl_stack_backward(_ptr(gst), _ptr(co), b, c, h, w, h, w, r, 0, h, w, 0,
                                                       _ptr(g1), _ptr(g2), _stream(gst)), "rmd_dicl_stack_backward")
     res = {}
-    for v in ("px1", "0", "px4", "1", "2", "3", "4", "0"):
-        os.environ["RMD_DICL_BWD_PX"] = {"0": "0", "px4": "4"}.get(v, "1")     # ablations run on the 1-pixel kernel
+    for v in ("px1", "nochain", "0", "px4", "1", "2", "3", "4", "0"):
+        os.environ["RMD_DICL_BWD_PX"] = {"0": "0", "nochain": "0", "px4": "4"}.get(v, "1")     # ablations: 1-pixel kernel
+        os.environ["RMD_DICL_BWD_CHAIN"] = "1" if v == "nochain" else "0"
         os.environ["RMD_DICL_BWD_ABL"] = v if v in ("1", "2", "3", "4") else "0"
         for _ in range(3):
             fn()
