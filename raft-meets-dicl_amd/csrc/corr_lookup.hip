@@ -6,7 +6,8 @@
 // window reads exactly the (2r+2)^2 integer patch [x0-r, x0+r+1] x [y0-r, y0+r+1] of p's own
 // level-i map.
 //
-// gfx950 design: one lane per (query, level), 64 consecutive queries per wave, so
+// gfx950 design: one lane per (query, level, third of the window's output rows), 64
+// consecutive queries per wave, so
 // every output store (one channel, 64 queries) is a coalesced 256-byte row of the
 // (B, L*(2r+1)^2, H, W) result.  Each patch row is fetched as whole row chunks (16 B for fp16 at
 // levels 0-1) — 2 or 3 vector loads per row instead of 2r+2 scalar loads — and aligned with a
@@ -118,21 +119,29 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
 
 // ABL (diagnostic, RMD_ABLATE env, fp16/r=4 only): 0 normal, 1 = outputs to one channel slot
 // (no output HBM traffic), 2 = no pyramid loads (zero patch)
-template <typename T, int R, int L, int ABL = 0, int NT = 0>
+// PR (A/B knob RMD_LOOKUP_SPLIT): output rows per lane.  PR == D is one lane per (query, level);
+// PR < D splits a window's D output rows over ceil(D/PR) lanes (part = 0, 1, ...), each loading
+// PR+1 patch rows: more waves in flight for the same stores, at +1 patch row per extra part.
+template <typename T, int R, int L, int ABL = 0, int NT = 0, int PR = 2 * R + 1>
 __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const PyrGeom& g, int b, int p, int N,
                                              float x, float y, unsigned zmask, float* __restrict__ o,
-                                             bool active) {
+                                             bool active, int part = 0) {
     constexpr int D = 2 * R + 1;
     constexpr int K = 2 * R + 2;
+    constexpr int KR = PR + 1;                                      // patch rows this lane loads
     const int lh = g.lh[L], lw = g.lw[L];
+    const int own0 = part * PR;                                     // first output row this part owns
+    const int bb0 = min(own0, D - PR);                              // first output row it computes
     if ((zmask >> L) & 1u) {
         if (active)
-            for (int c = 0; c < D * D; ++c) o[(size_t)c * N] = 0.f;
+            for (int c = 0; c < D * D; ++c)
+                if (c % D >= own0 && c % D < own0 + PR) o[(size_t)c * N] = 0.f;
         return;
     }
     if (lh < 2 || lw < 2) {     // the reference normalises by (size-1) = 0 -> NaN (raft.py:73-74)
         if (active)
-            for (int c = 0; c < D * D; ++c) o[(size_t)c * N] = __builtin_nanf("");
+            for (int c = 0; c < D * D; ++c)
+                if (c % D >= own0 && c % D < own0 + PR) o[(size_t)c * N] = __builtin_nanf("");
         return;
     }
     const float inv = 1.0f / (float)(1 << L);
@@ -151,7 +160,8 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
 
     float hprev[D];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
+    for (int jj = 0; jj < KR; ++jj) {
+        const int j = bb0 + jj;
         const int yy = ys + j;
         const bool row_ok = yy >= 0 && yy < lh;
         const int yc = min(max(yy, 0), lh - 1);
@@ -166,7 +176,7 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
         float hcur[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
-        if (j > 0 && active) {
+        if (jj > 0 && active && (PR == D || j - 1 >= own0)) {
             const int bb = j - 1;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
@@ -181,15 +191,16 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
     }
 }
 
-// grid: (query blocks, batch, level) — one lane per (query, level)
-template <typename T, int R, int ABL = 0, int NT = 0>
+// grid: (query blocks, batch, level + levels * part) — one lane per (query, level, row part)
+template <typename T, int R, int ABL = 0, int NT = 0, int PR = 2 * R + 1>
 __global__ void __launch_bounds__(kThreads)
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
     const int N = g.height * g.width;
     const int p = blockIdx.x * kThreads + threadIdx.x;
     const int b = blockIdx.y;
-    const int L = blockIdx.z;
+    const int L = (int)blockIdx.z % g.levels;
+    const int part = (int)blockIdx.z / g.levels;
     const bool active = p < N;
     const int pc = active ? p : N - 1;
     const float x = coords[((size_t)b * 2 + 0) * N + pc];
@@ -197,10 +208,10 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     constexpr int D = 2 * R + 1;
     float* o = out + ((size_t)b * g.levels + L) * D * D * N + pc;
     switch (L) {
-        case 0: lookup_level<T, R, 0, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        case 1: lookup_level<T, R, 1, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        case 2: lookup_level<T, R, 2, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
-        default: lookup_level<T, R, 3, ABL, NT>(pyr, g, b, pc, N, x, y, zmask, o, active); break;
+        case 0: lookup_level<T, R, 0, ABL, NT, PR>(pyr, g, b, pc, N, x, y, zmask, o, active, part); break;
+        case 1: lookup_level<T, R, 1, ABL, NT, PR>(pyr, g, b, pc, N, x, y, zmask, o, active, part); break;
+        case 2: lookup_level<T, R, 2, ABL, NT, PR>(pyr, g, b, pc, N, x, y, zmask, o, active, part); break;
+        default: lookup_level<T, R, 3, ABL, NT, PR>(pyr, g, b, pc, N, x, y, zmask, o, active, part); break;
     }
 }
 
@@ -223,6 +234,21 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
     // queries' row chunks re-read; nt loads lose exactly that reuse.
     const char* nt_env = getenv("RMD_LOOKUP_NT");
     const int nt = nt_env ? atoi(nt_env) : 1;
+    // RMD_LOOKUP_SPLIT (A/B, tools/lookup_ab.py + bench.py, profiles/lookup_split_r01.json): output rows
+    // per lane at r=4 — 9 (no split), 5, 3 (default: 3 parts, 12 patch rows loaded instead of 10), 2, 1.
+    // In the bench sequence (cfg2) 27.1 / 25.9 / 25.4 / 25.5 / 27.5 us: with one lane per (query, level)
+    // the grid is 3.5 waves per SIMD that load, then store, in lock step; 3 parts give the memory
+    // system 10.5 waves whose read and write phases overlap.
+    const char* sp_env = getenv("RMD_LOOKUP_SPLIT");
+    const int pr = sp_env ? atoi(sp_env) : 3;
+    if (radius == 4 && nt == 1 && (pr == 5 || pr == 3 || pr == 2 || pr == 1)) {
+        const dim3 gs(grid.x, grid.y, grid.z * ((9 + pr - 1) / pr));
+        if (pr == 5) corr_lookup_kernel<T, 4, 0, 1, 5><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+        else if (pr == 3) corr_lookup_kernel<T, 4, 0, 1, 3><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+        else if (pr == 2) corr_lookup_kernel<T, 4, 0, 1, 2><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+        else corr_lookup_kernel<T, 4, 0, 1, 1><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+        return check_launch("rmd_corr_lookup");
+    }
     if (radius == 4 && nt == 2) { corr_lookup_kernel<T, 4, 0, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
     if (radius == 4 && nt == 3) { corr_lookup_kernel<T, 4, 0, 3><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
     switch (radius) {

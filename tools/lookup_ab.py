@@ -2,7 +2,7 @@
 """A/B of the cfg2 lookup variants (RMD_LOOKUP_NT, read per launch: 0 plain, 1 non-temporal output
 stores, 2 non-temporal pyramid loads, 3 both) on bench.py's synthetic inputs: 12 lookups per
 round, HIP events around each lookup launch, variants interleaved; outputs compared bitwise with
-variant 0.  usage: python tools/lookup_ab.py [rounds] -> JSON on stdout"""
+variant 0.  A variant name "NT:PR" also sets RMD_LOOKUP_SPLIT=PR (output rows per lane).  usage: python tools/lookup_ab.py [rounds] -> JSON on stdout"""
 import json
 import os
 import sys
@@ -22,17 +22,22 @@ def main():
     f1, f2, coords = bench.synthetic(8, 256, 55, 128, 12, 1234, dev)
     names = os.environ.get("RMD_AB", "0,1,2,3").split(",")
     pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
-    os.environ["RMD_LOOKUP_NT"] = "0"
+    def select(n):
+        nt, _, pr = n.partition(":")
+        os.environ["RMD_LOOKUP_NT"] = nt
+        os.environ["RMD_LOOKUP_SPLIT"] = pr or "9"
+
+    select("0")
     ref = [ops.corr_lookup(pyr, coords[i], 4) for i in range(12)]
     res = {}
     for n in names:
-        os.environ["RMD_LOOKUP_NT"] = n
+        select(n)
         res[n] = {"bitwise_equal_v0": all(torch.equal(ops.corr_lookup(pyr, coords[i], 4), ref[i]) for i in range(12))}
     del ref
     times = {n: [] for n in names}
     for _ in range(rounds):
         for n in names:
-            os.environ["RMD_LOOKUP_NT"] = n
+            select(n)
             ev = []
             for i in range(12):
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
