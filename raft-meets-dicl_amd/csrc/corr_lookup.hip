@@ -239,8 +239,11 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
     // In the bench sequence (cfg2) 27.1 / 25.9 / 25.4 / 25.5 / 27.5 us: with one lane per (query, level)
     // the grid is 3.5 waves per SIMD that load, then store, in lock step; 3 parts give the memory
     // system 10.5 waves whose read and write phases overlap.
+    // Every other radius splits into 3 parts too (PR = ceil((2r+1)/3)); RMD_LOOKUP_SPLIT=0 turns it off.
     const char* sp_env = getenv("RMD_LOOKUP_SPLIT");
     const int pr = sp_env ? atoi(sp_env) : 3;
+    const bool split = pr != 0 && pr != 2 * radius + 1;
+    const dim3 g3(grid.x, grid.y, grid.z * 3);
     if (radius == 4 && nt == 1 && (pr == 5 || pr == 3 || pr == 2 || pr == 1)) {
         const dim3 gs(grid.x, grid.y, grid.z * ((9 + pr - 1) / pr));
         if (pr == 5) corr_lookup_kernel<T, 4, 0, 1, 5><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
@@ -254,6 +257,7 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
     switch (radius) {
 #define RMD_CASE(RR) case RR: \
         if (nt == 0) corr_lookup_kernel<T, RR, 0, 0><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        else if (split) corr_lookup_kernel<T, RR, 0, 1, (2 * RR + 3) / 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); \
         else corr_lookup_kernel<T, RR, 0, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
         break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
