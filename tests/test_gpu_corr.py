@@ -67,6 +67,32 @@ def test_cfg1_shape_matches_oracle(precision):
     assert rel_max_err(out, ref) < TOL[precision]
 
 
+@pytest.mark.parametrize("radius", [1, 2, 3, 5, 6, 8])
+def test_lookup_every_radius_row_split_vs_oracle(radius):
+    """The lookup splits each window's 2r+1 output rows over 3 lanes (PR = ceil((2r+1)/3); for
+    r = 2, 3, 5, 6, 8 the last part overlaps the previous one and stores only its own rows).  Checks
+    every radius the kernel is built for against the oracle, with a masked level (zeros), a 1-pixel
+    level (NaN, raft.py:73-74) and coordinates far outside the map."""
+    import rmd
+    rng = np.random.default_rng(100 + radius)
+    f1 = rng.standard_normal((2, 32, 12, 20)).astype(np.float32)
+    f2 = rng.standard_normal((2, 32, 12, 20)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(12), np.arange(20), indexing="ij")
+    co = (np.stack([xs, ys])[None] + rng.normal(0, 3, (2, 2, 12, 20))).astype(np.float32)
+    co[1, :, 3:5, 7:11] += 40.0
+    for precision in ("fp32", "bf16"):
+        cb = rmd.raft.CorrBlock(_t(f1), _t(f2), 4, radius, precision=precision)
+        out = cb(_t(co), [4]).cpu().numpy()
+        ref = oracle.corr_lookup(oracle.corr_pyramid(f1.astype(np.float64), f2.astype(np.float64), 4),
+                                 co.astype(np.float64), radius, [4])
+        assert out.shape == ref.shape
+        assert np.array_equal(np.isnan(out), np.isnan(ref))
+        fin = ~np.isnan(ref)
+        d = (2 * radius + 1) ** 2
+        assert np.all(out[:, d:2 * d] == 0)                                # masked level 1
+        assert rel_max_err(out[fin], ref[fin]) < TOL[precision]
+
+
 def _cfg2_inputs(seed=5, b=8):
     rng = np.random.default_rng(seed)
     f1 = rng.standard_normal((b, 256, 55, 128)).astype(np.float32)
