@@ -22,7 +22,11 @@
 namespace rmd {
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef RMD_LOOKUP_THREADS
+#define RMD_LOOKUP_THREADS 64      // one wave per workgroup: 25.64 vs 25.89 us (256) in the bench sequence
+                                   // (profiles/lookup_threads_r01.json; A/B builds: tools/_gpu_threads.sh)
+#endif
+constexpr int kThreads = RMD_LOOKUP_THREADS;
 
 typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
