@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "bf16-f32", "fp32-f16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
+    ap.add_argument("--event-every", type=int, default=5,
+                    help="record the per-kernel HIP events (roofline) on every E-th timed step")
     return ap.parse_args()
 
 
@@ -162,8 +164,8 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i % max(1, args.event_every) == 0)
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     elapsed = job_time(elapsed, world, device)
