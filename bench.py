@@ -41,7 +41,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=8, help="frame pairs per GPU")
     ap.add_argument("--height", type=int, default=436)
     ap.add_argument("--width", type=int, default=1024)
@@ -53,8 +53,32 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
     ap.add_argument("--event-every", type=int, default=5,
-                    help="record the per-kernel HIP events (roofline) on every E-th timed step")
+                    help="record the per-kernel HIP events (roofline) on every E-th timed step "
+                         "(steps E-1, 2E-1, ...: never the first timed step)")
+    ap.add_argument("--model-level", choices=["auto", "on", "off"], default="auto",
+                    help="also time the whole RAFT network (436x1024 b8, 12 iterations) with the rmd path "
+                         "(extra key; auto = single-GPU runs only)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/collective plumbing only (no GPU work): for the CPU gloo tests")
     return ap.parse_args()
+
+
+def maybe_launch(args):
+    """`bench.py --gpus N` (N > 1) started as a plain process launches its own N ranks: one process
+    per GPU through torch.distributed.run (127.0.0.1 rendezvous), as the driver does; returns only
+    in a rank (or a single-GPU run).  Runs before anything touches the GPU; the child processes are
+    started with subprocess (no exec from this process)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
 
 
 def padded(h, w, mod=8):
@@ -79,28 +103,80 @@ def synthetic(b, c, h8, w8, iters, seed, device):
     return f1.to(device), f2.to(device), torch.stack(coords).to(device)
 
 
-def cpu_baseline(args, h8, w8):
-    """Oracle (numpy float32 restatement of raft.py:18-95) on one frame pair, this host's cores."""
-    import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", len(os.sched_getaffinity(0))))
-    rng = np.random.default_rng(0)
-    f1 = rng.standard_normal((1, args.channels, h8, w8)).astype(np.float32)
-    f2 = rng.standard_normal((1, args.channels, h8, w8)).astype(np.float32)
-    ys, xs = np.meshgrid(np.arange(h8, dtype=np.float32), np.arange(w8, dtype=np.float32), indexing="ij")
-    co = (np.stack([xs, ys])[None] + rng.normal(0, 4, (1, 2, h8, w8))).astype(np.float32)
-    pairs = 0
-    t0 = time.perf_counter()
-    while True:
-        pyr = oracle.corr_pyramid(f1, f2, args.levels)
-        for _ in range(args.iters):
-            oracle.corr_lookup(pyr, co, args.radius)
-        pairs += 1
-        el = time.perf_counter() - t0
-        if el > args.cpu_budget_s:
-            break
-    return {"value": pairs / el, "unit": "frame-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{pairs} frame pair(s) of the same workload (1x{args.channels}x{h8}x{w8}, "
-                      f"pyramid + {args.iters} lookups), oracle/ numpy+BLAS float32, {el:.1f} s"}
+def cpu_baseline(args):
+    """BASELINE configs[0] on this host's cores: the whole RAFT network (raft/baseline, 12 GRU
+    iterations, synthetic 368x496 pair, batch 1, fp32) with the reference's eager correlation
+    (tests/e2e/eager_corr.EagerCorrBlock = raft.py:15-95 op for op) on torch-CPU; 1 warm-up, median of
+    5.  Test infrastructure timed as the baseline, never the product path."""
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from detinit import det_init_fanin
+    from e2e.eager_corr import EagerCorrBlock
+    from e2e.raft_net import RaftNet
+    from synth import frame_pair
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        net = det_init_fanin(RaftNet(EagerCorrBlock)).eval()
+        img1, img2, _ = frame_pair(368, 496)
+        i1, i2 = torch.from_numpy(img1), torch.from_numpy(img2)
+        times = []
+        with torch.no_grad():
+            for k in range(6):
+                t0 = time.perf_counter()
+                net(i1, i2, 12)
+                if k:
+                    times.append(time.perf_counter() - t0)
+                if k and sum(times) > args.cpu_budget_s * 3:
+                    break
+    finally:
+        torch.set_num_threads(prev)
+    med = float(np.median(times))
+    return {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": threads, "kind": "port",
+            "ms_per_pair": med * 1e3, "runs": len(times),
+            "sample": f"BASELINE configs[0]: whole RAFT network (raft/baseline, 12 iterations) on one synthetic "
+                      f"368x496 pair, batch 1, fp32 torch-CPU with the reference's eager correlation "
+                      f"(tests/e2e/eager_corr.py); 1 warm-up + median of {len(times)}"}
+
+
+def model_level(rank_dev, precision):
+    """Context for the headline (not `value`): the whole RAFT network at 436x1024 (padded 440x1024),
+    batch 8, 12 iterations, MIOpen fp32 convolutions, with rmd.raft.CorrBlock + rmd.raft.Up8Network
+    (tools/bench_e2e.py compares it with the eager reference correlation)."""
+    import torch.nn.functional as F
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import rmd
+    from detinit import det_init_fanin
+    from e2e.raft_net import RaftNet
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    b, h, w = 8, 440, 1024
+    g = torch.Generator().manual_seed(1234)
+    low = torch.rand(b, 3, h // 8, w // 8, generator=g) * 2 - 1
+    img1 = F.interpolate(low, size=(h, w), mode="bilinear", align_corners=True).to(rank_dev)
+    img2 = torch.roll(img1, shifts=(3, 5), dims=(2, 3))
+    net = det_init_fanin(RaftNet(rmd.raft.CorrBlock, precision=precision, upnet_cls=rmd.raft.Up8Network))
+    net = net.eval().to(rank_dev)
+    with torch.no_grad():
+        for _ in range(2):
+            net(img1, img2, 12)
+        torch.cuda.synchronize(rank_dev)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            net(img1, img2, 12)
+        torch.cuda.synchronize(rank_dev)
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    del net
+    torch.cuda.empty_cache()
+    return {"frame_pairs_per_s": b * 1e3 / ms, "ms_per_batch": ms, "batch": b, "iterations": 12,
+            "precision": precision, "convs": "MIOpen fp32 (TF32 off)",
+            "workload": "whole RAFT network 436x1024 (padded 440x1024): encoders + GRU + rmd correlation + rmd Up8"}
 
 
 def job_time(elapsed, world, device):
@@ -120,102 +196,86 @@ def rank_inputs(args, rank, h8, w8, device):
     return synthetic(args.batch, args.channels, h8, w8, args.iters, 1234 + rank, device)
 
 
-def main():
-    args = parse()
+def init_distributed(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.dry_run:
+        device = torch.device("cpu")
+    else:
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        if device.type == "cuda" and args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
+        assert dist.get_world_size() == world
+    return world, rank, device
 
-    import rmd
-    from rmd import ops
 
+def main():
+    args = parse()
+    maybe_launch(args)
+    world, rank, device = init_distributed(args)
     H, W = padded(args.height, args.width)
     h8, w8 = H // 8, W // 8
     B = args.batch
-    f1, f2, coords = rank_inputs(args, rank, h8, w8, device)
+    N = h8 * w8
+    D = (2 * args.radius + 1) ** 2
 
-    stream = torch.cuda.current_stream(device)
     ev_gemm = []      # (start, end) around the GEMM launch alone (rmd_corr_pyramid_prepared)
     ev_look = []      # (start, end) around the 12 lookup launches of a step
+    if args.dry_run:
+        def step(record):
+            return None
+    else:
+        from rmd import ops
+        f1, f2, coords = rank_inputs(args, rank, h8, w8, device)
+        stream = torch.cuda.current_stream(device)
 
-    def step(record):
-        pyr = ops.corr_pyramid(f1, f2, args.levels, args.precision, events=ev_gemm if record else None)
-        if record:
-            a = torch.cuda.Event(enable_timing=True)
-            z = torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-        out = None
-        for it in range(args.iters):
-            out = ops.corr_lookup(pyr, coords[it], args.radius)
-        if record:
-            z.record(stream)
-            ev_look.append((a, z))
-        return out
+        def step(record):
+            pyr = ops.corr_pyramid(f1, f2, args.levels, args.precision, events=ev_gemm if record else None)
+            if record:
+                a = torch.cuda.Event(enable_timing=True)
+                z = torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+            out = None
+            for it in range(args.iters):
+                out = ops.corr_lookup(pyr, coords[it], args.radius)
+            if record:
+                z.record(stream)
+                ev_look.append((a, z))
+            return out
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize(device)
 
     for _ in range(args.warmup):
         step(False)
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize(device)
+    sync()
+    E = max(1, args.event_every)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i % max(1, args.event_every) == 0)
-    torch.cuda.synchronize(device)
+        step(i % E == E - 1)
+    sync()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
     elapsed = job_time(elapsed, world, device)
 
-    gemm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_gemm]))
-    look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look])) / args.iters
-    N = h8 * w8
-    D = (2 * args.radius + 1) ** 2
     s = 2 if args.precision in ("bf16", "fp32-f16") else 4
-    levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
-    # algorithmic bytes
-    look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
-    op_bytes = 2 if args.precision.startswith("bf16") else 4
-    gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
-    gemm_flop = 2.0 * B * N * N * args.channels
     compute_dt = "fp32" if args.precision.startswith("fp32") else "bf16"
-    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
-    gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
-    gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
-
-    pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as fh:
-                pmc = json.load(fh).get(args.precision, {})
-        except (OSError, ValueError):
-            pmc = {}
-    roof_gemm = {"kernel": "corr_pyramid_w8 (bf16 MFMA GEMM + fused pooled-pyramid epilogue)",
-                 "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
-                 "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
-                 "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[compute_dt],
-                 "mfma_frac": gemm_tfs / MFMA_PEAK[compute_dt], "algorithmic_flop_per_launch": gemm_flop}
-    roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
-                 "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
-                 "traffic": pmc.get("lookup_hbm_bytes_per_launch"),
-                 "algorithmic_bytes_per_launch": look_bytes, "avg_launch_ms": look_ms,
-                 "launches_per_step": args.iters}
-    dominant_gemm = gemm_ms >= look_ms * args.iters
-
-    if rank != 0:
-        if world > 1:
-            torch.distributed.destroy_process_group()
-        return
-
-    total_pairs = world * B * args.steps
     res = {
         "metric": "frame-pairs/s @436x1024 RAFT 12 iters (1-8 GPU); corr MFMA% + lookup HBM%",
-        "value": total_pairs / elapsed,
+        "value": world * B * args.steps / elapsed,
         "unit": "frame-pairs/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -232,13 +292,56 @@ def main():
                    "channels": args.channels, "batch_per_gpu": B, "global_batch": B * world,
                    "lookups_per_step": args.iters, "precision": args.precision,
                    "pyramid_storage": "fp16" if s == 2 else "fp32", "parallelism": f"batch-shard x{world}"},
-        "roofline": roof_gemm if dominant_gemm else roof_look,
-        "roofline_gemm": roof_gemm,
-        "roofline_lookup": roof_look,
     }
-    if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args, h8, w8)
-    print(json.dumps(res), flush=True)
+    if args.dry_run:
+        res["dry_run"] = "launcher / collective plumbing only: no GPU work, value meaningless"
+    else:
+        gemm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_gemm]))
+        look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look])) / args.iters
+        levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
+        # algorithmic bytes
+        look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
+        op_bytes = 2 if args.precision.startswith("bf16") else 4
+        gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
+        gemm_flop = 2.0 * B * N * N * args.channels
+        look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+        gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
+        gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
+        pmc = {}
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_r02.json")
+        if not os.path.exists(pmc_path):
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+        if os.path.exists(pmc_path):
+            try:
+                with open(pmc_path) as fh:
+                    pmc = json.load(fh).get(args.precision, {})
+            except (OSError, ValueError):
+                pmc = {}
+        from rmd import _lib
+        kname = _lib.lib().rmd_corr_gemm_kernel(_lib.describe(B, h8, w8, args.levels, _lib.RMD_F16 if s == 2 else _lib.RMD_F32),
+                                                 args.channels, _lib.RMD_BF16 if compute_dt == "bf16" else _lib.RMD_F32)
+        roof_gemm = {"kernel": f"corr_pyramid_{kname.decode()} (MFMA GEMM + fused pooled-pyramid epilogue)",
+                     "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
+                     "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
+                     "event_samples": len(ev_gemm),
+                     "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[compute_dt],
+                     "mfma_frac": gemm_tfs / MFMA_PEAK[compute_dt], "algorithmic_flop_per_launch": gemm_flop}
+        roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
+                     "traffic": pmc.get("lookup_hbm_bytes_per_launch"),
+                     "algorithmic_bytes_per_launch": look_bytes, "avg_launch_ms": look_ms,
+                     "launches_per_step": args.iters, "event_samples": len(ev_look)}
+        dominant_gemm = gemm_ms >= look_ms * args.iters
+        res["roofline"] = roof_gemm if dominant_gemm else roof_look
+        res["roofline_gemm"] = roof_gemm
+        res["roofline_lookup"] = roof_look
+        if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
+            res["model_level"] = model_level(device, args.precision)
+    if rank == 0:
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

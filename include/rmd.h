@@ -89,6 +89,12 @@ int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, float
                      const rmd_pyramid_desc* desc, int compute, void* pyramid, void* workspace,
                      void* stream);
 
+/* Name of the GEMM kernel rmd_corr_pyramid runs for these arguments: "w8" (bf16 operands, fp16
+ * pyramid, C <= 256: the performance path), "stationary" (the same with 64-bit store addressing, for
+ * maps whose level-0 row span passes 1 GiB, e.g. 4K frames), "tiled" (exact f32 MFMA or any other
+ * combination), or "invalid".  Host-only; for tests and introspection. */
+const char* rmd_corr_gemm_kernel(const rmd_pyramid_desc* desc, int channels, int compute);
+
 /* The two halves of rmd_corr_pyramid, for callers that time or overlap them separately:
  * rmd_corr_prepare transposes/converts both feature maps into the workspace (pixel-major,
  * channel-contiguous operands); rmd_corr_pyramid_prepared runs the GEMM + pyramid epilogue on them. */

@@ -17,8 +17,6 @@
 
 #include "rmd_common.h"
 
-#include <cstdlib>
-
 namespace rmd {
 namespace {
 
@@ -121,7 +119,7 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
     }
 }
 
-// ABL (diagnostic, RMD_ABLATE env, fp16/r=4 only): 0 normal, 1 = outputs to one channel slot
+// ABL (diagnostic build only, RMD_ABLATE env, fp16/r=4): 0 normal, 1 = outputs to one channel slot
 // (no output HBM traffic), 2 = no pyramid loads (zero patch)
 // PR (A/B knob RMD_LOOKUP_SPLIT): output rows per lane.  PR == D is one lane per (query, level);
 // PR < D splits a window's D output rows over ceil(D/PR) lanes (part = 0, 1, ...), each loading
@@ -226,43 +224,46 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
     dim3 grid((N + kThreads - 1) / kThreads, d.batch, d.levels);
     const T* p = reinterpret_cast<const T*>(pyr);
     const PyrGeom g = make_geom(d);
-    const char* abl_env = getenv("RMD_ABLATE");
-    const int abl = abl_env ? atoi(abl_env) : 0;
-    if constexpr (sizeof(T) == 2) {
-        if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
-        if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+#ifdef RMD_DIAG
+    // A/B variants (tools/lookup_ab.py, librmd_diag.so only):
+    //  RMD_ABLATE (fp16, r = 4): 1 = outputs to one channel slot, 2 = no pyramid loads (results wrong)
+    //  RMD_LOOKUP_NT: 0 plain, 1 (product) nt output stores, 2 nt pyramid loads, 3 both.  cfg2
+    //    (profiles/lookup_ab_r01.json): 27.1 / 24.4 / 36.6 / 36.8 us — the 73 MB output is written
+    //    once and must not evict the pyramid lines that neighbouring queries' row chunks re-read.
+    //  RMD_LOOKUP_SPLIT (r = 4): output rows per lane, 9 (no split) / 5 / 3 (product) / 2 / 1 —
+    //    27.1 / 25.9 / 25.4 / 25.5 / 27.5 us in the bench sequence (profiles/lookup_split_r01.json).
+    {
+        const int abl = env_knob("RMD_ABLATE", 0);
+        const int nt = env_knob("RMD_LOOKUP_NT", 1);
+        const int pr = env_knob("RMD_LOOKUP_SPLIT", 3);
+        if constexpr (sizeof(T) == 2) {
+            if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+            if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+        }
+        if (radius == 4 && nt == 1 && pr != 3) {
+            const dim3 gs(grid.x, grid.y, grid.z * ((9 + pr - 1) / pr));
+            if (pr == 5) corr_lookup_kernel<T, 4, 0, 1, 5><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            else if (pr == 2) corr_lookup_kernel<T, 4, 0, 1, 2><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            else if (pr == 1) corr_lookup_kernel<T, 4, 0, 1, 1><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            else corr_lookup_kernel<T, 4, 0, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            return check_launch("rmd_corr_lookup");
+        }
+        if (radius == 4 && nt != 1) {
+            if (nt == 0) corr_lookup_kernel<T, 4, 0, 0><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            else if (nt == 2) corr_lookup_kernel<T, 4, 0, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            else corr_lookup_kernel<T, 4, 0, 3><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out);
+            return check_launch("rmd_corr_lookup");
+        }
     }
-    // RMD_LOOKUP_NT (A/B, tools/lookup_ab.py): 0 plain, 1 (default) non-temporal output stores,
-    // 2 nt pyramid loads, 3 both.  cfg2 (profiles/lookup_ab_r01.json): 27.1 / 24.4 / 36.6 / 36.8 us —
-    // the 73 MB output is written once and must not evict the pyramid lines that neighbouring
-    // queries' row chunks re-read; nt loads lose exactly that reuse.
-    const char* nt_env = getenv("RMD_LOOKUP_NT");
-    const int nt = nt_env ? atoi(nt_env) : 1;
-    // RMD_LOOKUP_SPLIT (A/B, tools/lookup_ab.py + bench.py, profiles/lookup_split_r01.json): output rows
-    // per lane at r=4 — 9 (no split), 5, 3 (default: 3 parts, 12 patch rows loaded instead of 10), 2, 1.
-    // In the bench sequence (cfg2) 27.1 / 25.9 / 25.4 / 25.5 / 27.5 us: with one lane per (query, level)
-    // the grid is 3.5 waves per SIMD that load, then store, in lock step; 3 parts give the memory
-    // system 10.5 waves whose read and write phases overlap.
-    // Every other radius splits into 3 parts too (PR = ceil((2r+1)/3)); RMD_LOOKUP_SPLIT=0 turns it off.
-    const char* sp_env = getenv("RMD_LOOKUP_SPLIT");
-    const int pr = sp_env ? atoi(sp_env) : 3;
-    const bool split = pr != 0 && pr != 2 * radius + 1;
+#endif
+    // Product path: non-temporal output stores, and every radius splits a window's 2r+1 output rows
+    // over 3 lanes (PR = floor((2r+3)/3) rows each, ceil((2r+1)/PR) = 3 for r = 1..8): with one lane
+    // per (query, level) the cfg2 grid is 3.5 waves per SIMD that load, then store, in lock step; 3
+    // parts give the memory system 10.5 waves whose read and write phases overlap.
     const dim3 g3(grid.x, grid.y, grid.z * 3);
-    if (radius == 4 && nt == 1 && (pr == 5 || pr == 3 || pr == 2 || pr == 1)) {
-        const dim3 gs(grid.x, grid.y, grid.z * ((9 + pr - 1) / pr));
-        if (pr == 5) corr_lookup_kernel<T, 4, 0, 1, 5><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
-        else if (pr == 3) corr_lookup_kernel<T, 4, 0, 1, 3><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
-        else if (pr == 2) corr_lookup_kernel<T, 4, 0, 1, 2><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
-        else corr_lookup_kernel<T, 4, 0, 1, 1><<<gs, kThreads, 0, st>>>(p, g, coords, zmask, out);
-        return check_launch("rmd_corr_lookup");
-    }
-    if (radius == 4 && nt == 2) { corr_lookup_kernel<T, 4, 0, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
-    if (radius == 4 && nt == 3) { corr_lookup_kernel<T, 4, 0, 3><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
     switch (radius) {
 #define RMD_CASE(RR) case RR: \
-        if (nt == 0) corr_lookup_kernel<T, RR, 0, 0><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
-        else if (split) corr_lookup_kernel<T, RR, 0, 1, (2 * RR + 3) / 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); \
-        else corr_lookup_kernel<T, RR, 0, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        corr_lookup_kernel<T, RR, 0, 1, (2 * RR + 3) / 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); \
         break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE

@@ -471,11 +471,11 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     const size_t lds = sizeof(float) * kQ * kLd;
     const size_t qn = otf_query_elems(g);
     // compiled channel counts keep the query segments in registers; f32 operands of >= 128 channels
-    // would not fit and take the runtime loop (RMD_OTF_RUNTIME=1 forces it for A/B runs)
-    // RMD_OTF_ABLATE (diagnostics only, results invalid): bits 1 = skip output stores, 2 = skip the MFMA
+    // would not fit and take the runtime loop (RMD_OTF_RUNTIME=1 forces it in the diagnostic build)
+    // RMD_OTF_ABLATE (diagnostic build only, results invalid): bits 1 = skip output stores, 2 = skip the MFMA
     // phase
-    static const int ablate = getenv("RMD_OTF_ABLATE") ? atoi(getenv("RMD_OTF_ABLATE")) : 0;
-    static const bool force_rt = getenv("RMD_OTF_RUNTIME") && atoi(getenv("RMD_OTF_RUNTIME")) != 0;
+    const int ablate = env_knob("RMD_OTF_ABLATE", 0);           // always 0 outside librmd_diag.so
+    const bool force_rt = env_knob("RMD_OTF_RUNTIME", 0) != 0;
     const int cpt = force_rt || (compute == RMD_F32 && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
 #define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \

@@ -850,6 +850,7 @@ __device__ __forceinline__ void phase(f32x16 (&accM)[8], const f32x16 (&accE)[8]
 
 }  // namespace pipe
 
+#ifdef RMD_DIAG   // software-pipelined 4-wave variant: A/B only (tools/gemm_ab.py, librmd_diag.so)
 __global__ void __launch_bounds__(256, 1)
 corr_pyramid_pipe(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
                   __half* __restrict__ pyr, int drop_stores) {
@@ -942,6 +943,7 @@ corr_pyramid_pipe(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB
         pipe::phase<true, true>(accA, accB, bq, smem, arow, h, qrow(k + 2), c, qidx(min(k, n - 1)), k < n);
     }
 }
+#endif  // RMD_DIAG
 
 // ---------------------------------------------------------------------------------------------
 // 8-wave target-stationary kernel (bf16 operands, fp16 pyramid, C = 256).
@@ -1058,7 +1060,11 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
         const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 2u : 0u;
         const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;
+#ifdef RMD_DIAG
+        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;    // ablation: drop every store
+#else
+        const unsigned range = (unsigned)rows * rs;
+#endif
         __half* bp = pyr + base;
         const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
         const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
@@ -1083,11 +1089,16 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
 #pragma unroll
         for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 512 * s);
     }
-    // diagnostic knobs: stagger % 1000 = s_sleep(16) count that desynchronises the two waves of each
-    // SIMD; stagger >= 1000 = static s_setprio 1 for the second-dispatched half (waves 4-7)
+#ifdef RMD_DIAG
+    // A/B knobs: stagger % 1000 = s_sleep(16) count that desynchronises the two waves of each SIMD;
+    // stagger >= 1000 = static s_setprio 1 for the second-dispatched half (waves 4-7)
     if ((stagger % 1000) && w >= 4)
         for (int i = 0; i < stagger % 1000; ++i) __builtin_amdgcn_s_sleep(16);
     if (stagger >= 1000 && w >= 4) __builtin_amdgcn_s_setprio(1);
+#else
+    (void)drop_stores;
+    (void)stagger;
+#endif
     while (true) {
         f32x16 acc[8];
         const int qn = qt + stride;
@@ -1109,21 +1120,24 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
     }
 }
 
-// GEMM path for a call: the w8 kernel (default) needs bf16 operands, an fp16 pyramid, C <= 256 and
-// 32-bit store offsets; RMD_GEMM_KERNEL = pipe | stationary | tiled selects the others (diagnostic).
+// GEMM path for a call: the w8 kernel needs bf16 operands, an fp16 pyramid, C <= 256 and 32-bit
+// store offsets (one wave's 16 level-0 rows < 1 GiB); larger maps (e.g. 4K frames) take the
+// stationary kernel (64-bit addressing), everything else the tiled kernel.  The diagnostic build
+// also honours RMD_GEMM_KERNEL = pipe | stationary | tiled.
 enum class Path { W8, PIPE, STATIONARY, TILED };
 
 Path gemm_path(const rmd_pyramid_desc& d, int C, int compute) {
     const int Cp = (C + kKC - 1) / kKC * kKC;
+    if (compute != RMD_BF16 || d.storage != RMD_F16 || Cp != 256) return Path::TILED;
+#ifdef RMD_DIAG
     const char* k_env = getenv("RMD_GEMM_KERNEL");
-    if (compute != RMD_BF16 || d.storage != RMD_F16 || Cp != 256 || getenv("RMD_FORCE_TILED_GEMM") ||
-        (k_env && strcmp(k_env, "tiled") == 0))
-        return Path::TILED;
+    if (k_env && strcmp(k_env, "tiled") == 0) return Path::TILED;
+    if (k_env && strcmp(k_env, "stationary") == 0) return Path::STATIONARY;
+    if (k_env && strcmp(k_env, "pipe") == 0) return Path::PIPE;
+#endif
     const long long N = (long long)d.height * d.width;
     const double span0 = 16.0 * d.tiles_x[0] * (double)N * 8 * 2;     // one wave's 16 level-0 rows (bytes)
     if (span0 >= (double)(1u << 30)) return Path::STATIONARY;
-    if (k_env && strcmp(k_env, "stationary") == 0) return Path::STATIONARY;
-    if (k_env && strcmp(k_env, "pipe") == 0) return Path::PIPE;
     return Path::W8;
 }
 
@@ -1174,34 +1188,33 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
             __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * nqt * 32 * Cp);
             const Path path = gemm_path(d, C, RMD_BF16);
             if (path == Path::W8) {
-                const char* ab = getenv("RMD_ABLATE");
                 // stores are non-temporal (aux bit 1, nt): measured 0.24 vs 0.26 ms plain at cfg2 (the
-                // pyramid is written once and read back a full GEMM later); RMD_STORE_AUX overrides
-                const char* aux_env = getenv("RMD_STORE_AUX");
-                const int aux = aux_env ? atoi(aux_env) : 2;
+                // pyramid is written once and read back a full GEMM later)
                 int qs = 1;
                 while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
-                const char* roll_env = getenv("RMD_W8_ROLL");
-                const char* stag_env = getenv("RMD_W8_STAGGER");
-                const bool roll = roll_env && atoi(roll_env);
-                const int stagger = stag_env ? atoi(stag_env) : 0;
-                auto kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true> : corr_pyramid_w8<2, false>)
-                                     : (roll ? corr_pyramid_w8<0, true> : corr_pyramid_w8<0, false>);
+                auto kern = corr_pyramid_w8<2, false>;
+                int drop = 0, stagger = 0;
+#ifdef RMD_DIAG
+                const int aux = env_knob("RMD_STORE_AUX", 2);
+                const bool roll = env_knob("RMD_W8_ROLL", 0) != 0;
+                kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true> : corr_pyramid_w8<2, false>)
+                                : (roll ? corr_pyramid_w8<0, true> : corr_pyramid_w8<0, false>);
+                drop = env_knob("RMD_ABLATE", 0) == 1;
+                stagger = env_knob("RMD_W8_STAGGER", 0);
+#endif
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, ab && atoi(ab) == 1, stagger);
+                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, drop, stagger);
                 return check_launch("rmd_corr_pyramid/gemm-w8");
             }
+#ifdef RMD_DIAG
             if (path == Path::PIPE) {
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_pipe),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                const char* ab = getenv("RMD_ABLATE");
-                corr_pyramid_pipe<<<nwg, 256, lds, st>>>(opA, opB, geom, qsplit, out, ab && atoi(ab) == 1);
+                corr_pyramid_pipe<<<nwg, 256, lds, st>>>(opA, opB, geom, qsplit, out, env_knob("RMD_ABLATE", 0) == 1);
                 return check_launch("rmd_corr_pyramid/gemm-pipe");
             }
-            const char* abl_env = getenv("RMD_ABLATE");
-            const int abl = abl_env ? atoi(abl_env) : 0;
-            const char* w_env = getenv("RMD_GEMM_WAVES");           // 4 (default) or 8
-            const int th = (w_env && atoi(w_env) == 8) ? 1 : 2;
+            const int abl = env_knob("RMD_ABLATE", 0);
+            const int th = env_knob("RMD_GEMM_WAVES", 4) == 8 ? 1 : 2;     // 4 (default) or 8 waves
             switch (th * 4 + (abl >= 0 && abl <= 2 ? abl : 0)) {
 #define RMD_SCASE(TH, ABL)                                                                                      \
     case TH * 4 + ABL:                                                                                          \
@@ -1212,6 +1225,11 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                 RMD_SCASE(1, 0) RMD_SCASE(1, 1) RMD_SCASE(1, 2) RMD_SCASE(2, 0) RMD_SCASE(2, 1) RMD_SCASE(2, 2)
 #undef RMD_SCASE
             }
+#else
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<2, 0>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            corr_pyramid_stationary<2, 0><<<nwg, STraits<2>::kThreads, lds, st>>>(opA, opB, geom, qsplit, out, trash);
+#endif
             return check_launch("rmd_corr_pyramid/gemm-stationary");
         }
     }
@@ -1241,6 +1259,16 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     const size_t es = compute == RMD_F32 ? 4 : 2;
     const size_t N = (size_t)d->height * d->width, Npad = (N + 31) / 32 * 32;   // B operand padded to 32-query tiles
     return (size_t)d->batch * (N + Npad) * Cp * es + 32 * 1024;                  // + trash slots (<= 32 x 1 KiB)
+}
+
+extern "C" const char* rmd_corr_gemm_kernel(const rmd_pyramid_desc* d, int channels, int compute) {
+    if (rmd::check_args(d, channels, compute) != RMD_OK) return "invalid";
+    switch (rmd::gemm_path(*d, channels, compute)) {
+        case rmd::Path::W8: return "w8";
+        case rmd::Path::PIPE: return "pipe";
+        case rmd::Path::STATIONARY: return "stationary";
+        default: return "tiled";
+    }
 }
 
 extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int channels, float scale,

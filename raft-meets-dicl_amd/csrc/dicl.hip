@@ -1331,6 +1331,7 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
             }
             return check_launch("rmd_dicl_stack_backward/patch4");
         }
+#ifdef RMD_DIAG
         const int abl = env_variant("RMD_DICL_BWD_ABL");     // diagnostic ablation (results wrong)
         if (radius == 4 && abl >= 1 && abl <= 4 && P.wl * 24 <= kWinSmall) {
             if (abl == 1) dicl_stack_patch_backward_kernel<4, kWinSmall, 1><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
@@ -1339,6 +1340,7 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
             if (abl == 4) dicl_stack_patch_backward_kernel<4, kWinSmall, 4><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
             return check_launch("rmd_dicl_stack_backward/patch-ablation");
         }
+#endif
         switch (radius) {
 #define RMD_CASE(RR) case RR: \
             if (small_win) dicl_stack_patch_backward_kernel<RR, kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
@@ -1418,7 +1420,7 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
                        float* out, void* stream) {
     RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");
     RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap: bad sizes");
-    if (disp <= 1024 && !getenv("RMD_DAP_VALU")) {
+    if (disp <= 1024 && !env_variant("RMD_DAP_VALU")) {
         const int Dk = (disp + 1) & ~1;
         const size_t lds = sizeof(float) * 32 * (size_t)(Dk + 1);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_kernel),

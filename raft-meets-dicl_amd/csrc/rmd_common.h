@@ -77,11 +77,23 @@ __device__ __forceinline__ int xcd_block(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-// diagnostic variant selector for A/B runs (env RMD_<NAME>, default 0); read on the host per launch
+// Diagnostic variant selector for A/B runs.  Only the diagnostic build (`make diag` ->
+// librmd_diag.so, -DRMD_DIAG; tools/ A/B scripts load it through RMD_LIBRARY) reads the
+// environment (RMD_<NAME>, default 0) and compiles the variant / ablation kernels; in the product
+// library every selector is the constant 0 and the alternatives are not compiled.
+#ifdef RMD_DIAG
 inline int env_variant(const char* name) {
     const char* v = getenv(name);
     return v ? atoi(v) : 0;
 }
+inline int env_knob(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+#else
+constexpr int env_variant(const char*) { return 0; }
+constexpr int env_knob(const char*, int dflt) { return dflt; }
+#endif
 
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }

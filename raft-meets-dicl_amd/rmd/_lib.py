@@ -46,6 +46,7 @@ _SIGS = {
     "rmd_corr_pyramid_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PyramidDesc), _I, _I]),
     "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_lookup": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
+    "rmd_corr_gemm_kernel": (ctypes.c_char_p, [ctypes.POINTER(PyramidDesc), _I, _I]),
     "rmd_corr_prepare": (_I, [_P, _P, _I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P]),
     "rmd_corr_pyramid_prepared": (_I, [_I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_otf_workspace_bytes": (ctypes.c_size_t, [_I] * 6),

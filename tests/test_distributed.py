@@ -128,3 +128,31 @@ def test_ddp_gradient_allreduce_through_corr_autograd():
         np.testing.assert_allclose(gw, ref_w, rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(gb, ref_b, rtol=1e-4, atol=1e-6)
     assert np.abs(ref_w).max() > 0
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_its_own_ranks(world):
+    """`bench.py --gpus N` started as one plain process spawns N ranks through
+    torch.distributed.run (the same launcher the driver uses) and reports n_gpus = the world size
+    the process group reports.  --dry-run skips the GPU work (gloo on CPU here)."""
+    import json
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dry-run",
+                          "--backend", "gloo", "--no-cpu-baseline", "--steps", "2", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout                      # rank 0 alone prints the JSON line
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == world and res["config"]["global_batch"] == 8 * world
+    assert res["steps"] == 2 and res["scaling"] == "weak"
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run",
+                          "--no-cpu-baseline"], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr

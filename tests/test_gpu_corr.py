@@ -120,6 +120,45 @@ def test_cfg2_full_size_sampled_queries(precision):
     assert rel_max_err(out[:, :, sel], ref.reshape(b, 324, -1)) < TOL[precision]
 
 
+def test_stationary_path_4k_sampled_vs_oracle():
+    """A 4K frame's 1/8-resolution map (2160x3840 -> 270x480, C=256, B=1): one wave's 16 level-0
+    rows exceed 32-bit store offsets, so the bf16 GEMM routes to corr_pyramid_stationary (64-bit
+    addressing, hand-placed vmcnt window audited in tests/test_asm_audit.py).  Pyramid 44.6 GB fp16;
+    oracle on 256 sampled queries, flow up to +-40 px, image corners included."""
+    import rmd
+    from rmd import _lib
+    h, w = 270, 480
+    d = _lib.describe(1, h, w, 4, _lib.RMD_F16)
+    assert _lib.lib().rmd_corr_gemm_kernel(d, 256, _lib.RMD_BF16) == b"stationary"
+    rng = np.random.default_rng(17)
+    f1 = rng.standard_normal((1, 256, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((1, 256, h, w)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    flow = rng.normal(0, 15, (1, 2, 1, 1)) + rng.normal(0, 8, (1, 2, h, w))
+    co = (np.stack([xs, ys])[None] + flow).astype(np.float32)
+    cb = rmd.raft.CorrBlock(_t(f1), _t(f2), 4, 4, precision="bf16")
+    out = cb(_t(co))
+    sel = np.sort(rng.choice(h * w, 256, replace=False))
+    sel[:4] = [0, w - 1, (h - 1) * w, h * w - 1]
+    got = out.reshape(1, 324, h * w)[:, :, torch.from_numpy(sel).to(DEV)].cpu().numpy()
+    del out, cb
+    torch.cuda.empty_cache()
+    f1s = f1.reshape(1, 256, h * w)[:, :, sel][:, :, None, :].astype(np.float64)
+    cos = co.reshape(1, 2, h * w)[:, :, sel][:, :, None, :].astype(np.float64)
+    ref = oracle.corr_lookup(oracle.corr_pyramid(f1s, f2.astype(np.float64), 4), cos, 4)
+    assert rel_max_err(got, ref.reshape(1, 324, -1)) < TOL["bf16"]
+
+
+def test_gemm_kernel_routing():
+    """cfg2 bf16 -> w8, fp32 -> tiled (exact f32 MFMA), 4K bf16 -> stationary."""
+    from rmd import _lib
+    lib = _lib.lib()
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F16), 256, _lib.RMD_BF16) == b"w8"
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F32), 256, _lib.RMD_F32) == b"tiled"
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F16), 128, _lib.RMD_BF16) == b"tiled"
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(1, 270, 480, 4, _lib.RMD_F16), 256, _lib.RMD_BF16) == b"stationary"
+
+
 def test_lookup_deterministic_and_pyramid_reusable():
     import rmd
     f1, f2, co = _cfg2_inputs(seed=9, b=2)

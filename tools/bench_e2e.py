@@ -22,40 +22,11 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
-class EagerCorrBlock:
-    """raft.CorrBlock (raft.py:15-95) in eager torch — the reference GPU path."""
-
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, precision=None):
-        self.num_levels, self.radius = num_levels, radius
-        b, c, h, w = fmap1.shape
-        corr = torch.matmul(fmap1.view(b, c, h * w).transpose(1, 2), fmap2.view(b, c, h * w))
-        corr = (corr / torch.tensor(c).float().sqrt()).view(b * h * w, 1, h, w)
-        self.pyr = [corr]
-        for _ in range(1, num_levels):
-            corr = F.avg_pool2d(corr, kernel_size=2, stride=2)
-            self.pyr.append(corr)
-
-    def __call__(self, coords, mask_costs=()):
-        r = self.radius
-        b, _, h, w = coords.shape
-        d = torch.linspace(-r, r, 2 * r + 1, device=coords.device)
-        delta = torch.stack(torch.meshgrid(d, d, indexing="ij"), dim=-1).view(1, 2 * r + 1, 2 * r + 1, 2)
-        co = coords.permute(0, 2, 3, 1).reshape(b * h * w, 1, 1, 2)
-        out = []
-        for i, corr in enumerate(self.pyr):
-            _, _, hh, ww = corr.shape
-            c = co / 2 ** i + delta
-            xg, yg = c.split(1, dim=-1)
-            grid = torch.cat((2 * xg / (ww - 1) - 1, 2 * yg / (hh - 1) - 1), dim=-1)
-            s = F.grid_sample(corr, grid, align_corners=True)
-            out.append(s.view(b, h, w, -1))
-        return torch.cat(out, dim=-1).permute(0, 3, 1, 2).contiguous().float()
-
-
 def main():
     import rmd
     from detinit import det_init_fanin
     from e2e.raft_net import RaftNet
+    from e2e.eager_corr import EagerCorrBlock
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     b = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     torch.backends.cudnn.allow_tf32 = False
