@@ -58,6 +58,12 @@ def parse():
     ap.add_argument("--model-level", choices=["auto", "on", "off"], default="auto",
                     help="also time the whole RAFT network (436x1024 b8, 12 iterations) with the rmd path "
                          "(extra key; auto = single-GPU runs only)")
+    ap.add_argument("--train", choices=["on", "off"], default="on",
+                    help="also time the cfg5 training step (RAFT+DICL ctf-l3, DDP over RCCL when N > 1): "
+                         "extra key 'train_step'")
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--train-batch", type=int, default=6, help="frame pairs per GPU (train/chairs2-1 stage)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/collective plumbing only (no GPU work): for the CPU gloo tests")
@@ -177,6 +183,85 @@ def model_level(rank_dev, precision):
     return {"frame_pairs_per_s": b * 1e3 / ms, "ms_per_batch": ms, "batch": b, "iterations": 12,
             "precision": precision, "convs": "MIOpen fp32 (TF32 off)",
             "workload": "whole RAFT network 436x1024 (padded 440x1024): encoders + GRU + rmd correlation + rmd Up8"}
+
+
+def train_leg(args, world, rank, device):
+    """BASELINE configs[4] / SURVEY.md §8(d) cfg5: one RAFT+DICL ctf-l3 training step per timed step —
+    synthetic FlyingChairs-shape pairs (368x496 padded to 384x512), per-GPU batch 6, iterations
+    (4, 3, 3), loss raft+dicl/mlseq (ord 1, gamma 0.85, alpha (0.38, 0.6, 1.0)), backward through the
+    HIP DICL stack / DAP / Up8 kernels, clip_grad_norm_(1.0), AdamW (lr one-cycle to 4e-4, weight decay
+    1e-4) — src/strategy/training.py:232-289.  N > 1: DistributedDataParallel over RCCL (bucketed
+    gradient all-reduce of the 12.68 M fp32 parameters, overlapped with backward), the replacement
+    of the reference's nn.DataParallel (src/cmd/train.py:183-184).  Network: tests/e2e/ctf_l3_net.py
+    (the reference's architecture and module names; encoders/GRU/MatchingNet are MIOpen convs)."""
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import rmd
+    from detinit import det_init_fanin
+    from e2e.ctf_l3_net import CtfL3Net, freeze_batchnorm, mlseq_loss
+    from synth import frame_pair
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    h, w, pad, bsz = 368, 496, 64, args.train_batch
+    net = det_init_fanin(CtfL3Net(rmd.corr.make_cmod, rmd.corr.make_flow_regression, upnet_cls=rmd.raft.Up8Network),
+                         head_gain=0.02).to(device)
+    n_params = sum(p.numel() for p in net.parameters())
+    net.train()
+    freeze_batchnorm(net)
+    model = net
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(net, device_ids=[device.index])
+    opt = torch.optim.AdamW(net.parameters(), lr=4e-4, weight_decay=1e-4, eps=1e-8)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=4e-4, total_steps=100000, pct_start=0.05,
+                                                cycle_momentum=False, anneal_strategy="linear")
+    i1s, i2s, fls, vas = [], [], [], []
+    for k in range(bsz):
+        seed = 1000 * rank + k
+        rng = np.random.default_rng(seed)
+        i1, i2, gt = frame_pair(h, w, flow=tuple(int(v) for v in rng.integers(0, 8, 2)), seed=seed, pad=pad)
+        hp, wp = i1.shape[-2:]
+        f = np.zeros((1, 2, hp, wp), np.float32)
+        f[:, :, :h, :w] = gt
+        v = np.zeros((1, hp, wp), bool)
+        v[:, :h, :w] = True
+        i1s.append(i1), i2s.append(i2), fls.append(f), vas.append(v)
+    img1, img2, flow, valid = (torch.from_numpy(np.concatenate(x)).to(device) for x in (i1s, i2s, fls, vas))
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = mlseq_loss(model(img1, img2, (4, 3, 3)), flow, valid)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(net.parameters(), 1.0, norm_type=2.0)
+        opt.step()
+        sched.step()
+        return loss
+
+    for _ in range(args.train_warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        loss = step()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    el = job_time(el, world, device)
+    last = float(loss)
+    del model, net, opt
+    torch.cuda.empty_cache()
+    return {"workload": "RAFT+DICL ctf-l3 training step (BASELINE configs[4], SURVEY cfg5): 368x496 padded "
+                        "384x512, iterations (4,3,3), mlseq loss, backward, clip 1.0, AdamW",
+            "frame_pairs_per_s": world * bsz * args.train_steps / el, "steps_per_s": args.train_steps / el,
+            "ms_per_step": el / args.train_steps * 1e3, "per_gpu_batch": bsz, "global_batch": world * bsz,
+            "n_gpus": world, "steps": args.train_steps, "warmup": args.train_warmup,
+            "parallelism": f"DDP x{world} (RCCL bucketed gradient all-reduce)" if world > 1 else "single GPU",
+            "gradient_bytes_per_step": 4 * n_params, "parameters": n_params, "last_loss": last,
+            "scaling": "weak", "dtype": "fp32", "data": "synthetic smooth pairs with known flow, name-keyed random weights"}
 
 
 def job_time(elapsed, world, device):
@@ -338,6 +423,10 @@ def main():
         res["roofline_lookup"] = roof_look
         if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
             res["model_level"] = model_level(device, args.precision)
+        if args.train == "on":
+            tr = train_leg(args, world, rank, device)      # every rank (DDP collectives)
+            if rank == 0:
+                res["train_step"] = tr
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args)
