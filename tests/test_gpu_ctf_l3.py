@@ -13,8 +13,10 @@ Tolerances:
     output (north_star's EPE gate); 1/32 and 1/16 flows of every iteration and sampled full-resolution
     flows within 1e-2 px (MIOpen vs CPU ATen convolutions: summation order only).
   * training step (cfg5 shape 384x512, batch 2, mlseq loss, clip 1.0, AdamW): loss and total gradient
-    norm within 1e-4 relative; every parameter's gradient norm within 1e-3 relative (or 1e-6 absolute
-    for near-zero gradients); the loss after the AdamW step within 1e-3 relative (the first Adam step
+    norm within 1e-4 relative; every parameter's gradient norm within 1e-3 relative, except gradients
+    that are zero in exact arithmetic and rounding noise in both runs (biases of convolutions followed
+    by InstanceNorm, e.g. fnet.conv1.bias: ~1e-6 against a total norm of ~2.6e3), which must stay below
+    1e-8 x the total norm; the loss after the AdamW step within 1e-3 relative (the first Adam step
     moves each weight by ~lr * sign(g), so near-zero gradients whose sign depends on summation order
     perturb it slightly).
 """
@@ -109,14 +111,18 @@ def test_ctf_l3_training_step_matches_reference():
     with torch.no_grad():
         loss1 = float(mlseq_loss(net(img1, img2, iters), flow, valid))
     ref_gn = g["grad_norms"]
+    noise = 1e-8 * float(g["grad_norm"])                 # rounding-noise level of exactly-zero gradients
+    zero = (ref_gn <= noise) & (gn <= noise)
     rel_gn = np.abs(gn - ref_gn) / np.maximum(np.abs(ref_gn), 1e-30)
-    ok_gn = (rel_gn <= 1e-3) | (np.abs(gn - ref_gn) <= 1e-6)
-    worst = int(np.argmax(np.where(np.abs(gn - ref_gn) <= 1e-6, 0, rel_gn)))
-    rep = {"loss": float(loss), "loss_ref": float(g["loss"]),
-           "loss_rel_diff": abs(float(loss) - float(g["loss"])) / abs(float(g["loss"])),
+    ok_gn = (rel_gn <= 1e-3) | zero
+    worst = int(np.argmax(np.where(zero, 0, rel_gn)))
+    loss = float(loss.detach())
+    rep = {"loss": loss, "loss_ref": float(g["loss"]),
+           "loss_rel_diff": abs(loss - float(g["loss"])) / abs(float(g["loss"])),
            "grad_norm": total, "grad_norm_ref": float(g["grad_norm"]),
            "grad_norm_rel_diff": abs(total - float(g["grad_norm"])) / float(g["grad_norm"]),
            "param_grad_norm_max_rel_diff": float(rel_gn[worst]), "worst_param": names[worst],
+           "zero_gradient_params": [names[i] for i in np.nonzero(zero)[0]],
            "loss_after_step": loss1, "loss_after_step_ref": float(g["loss_after_step"]),
            "loss_after_step_rel_diff": abs(loss1 - float(g["loss_after_step"])) / abs(float(g["loss_after_step"]))}
     _report("ctf_l3_train_step", rep)
