@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--radius", type=int, default=4)
     ap.add_argument("--levels", type=int, default=4)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "bf16-f32", "fp32-f16"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32-exact", "bf16-f32", "fp32-f16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
     ap.add_argument("--event-every", type=int, default=5,
@@ -389,6 +389,8 @@ def main():
         op_bytes = 2 if args.precision.startswith("bf16") else 4
         gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
         gemm_flop = 2.0 * B * N * N * args.channels
+        # MFMA work actually issued: the fp32 mode runs three bf16 products per k-step (x3 kernel)
+        mfma_dt, mfma_mult = ("bf16", 3.0) if args.precision == "fp32" else (compute_dt, 1.0)
         look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
         gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
         gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
@@ -403,15 +405,16 @@ def main():
             except (OSError, ValueError):
                 pmc = {}
         from rmd import _lib
-        kname = _lib.lib().rmd_corr_gemm_kernel(_lib.describe(B, h8, w8, args.levels, _lib.RMD_F16 if s == 2 else _lib.RMD_F32),
-                                                 args.channels, _lib.RMD_BF16 if compute_dt == "bf16" else _lib.RMD_F32)
+        kname = _lib.lib().rmd_corr_gemm_kernel(_lib.describe(B, h8, w8, args.levels, ops.PRECISIONS[args.precision][1]),
+                                                 args.channels, ops.PRECISIONS[args.precision][0])
         roof_gemm = {"kernel": f"corr_pyramid_{kname.decode()} (MFMA GEMM + fused pooled-pyramid epilogue)",
                      "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
                      "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
                      "event_samples": len(ev_gemm),
-                     "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[compute_dt],
-                     "mfma_frac": gemm_tfs / MFMA_PEAK[compute_dt], "algorithmic_flop_per_launch": gemm_flop}
+                     "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[mfma_dt],
+                     "mfma_frac": gemm_tfs * mfma_mult / MFMA_PEAK[mfma_dt], "mfma_products_per_flop": mfma_mult,
+                     "algorithmic_flop_per_launch": gemm_flop}
         roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
                      "traffic": pmc.get("lookup_hbm_bytes_per_launch"),

@@ -37,6 +37,7 @@ extern "C" {
 #define RMD_F32 0
 #define RMD_F16 1
 #define RMD_BF16 2
+#define RMD_BF16X3 3   /* compute only: fp32-accurate split bf16, hi.hi + hi.lo + lo.hi per k-step */
 
 #define RMD_MAX_LEVELS 4
 
@@ -80,8 +81,11 @@ size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* desc, int channe
  * levels-1 successive 2x2 average pools over the target dims, floor sizes.  scale = 1/sqrt(C) is
  * raft.CorrBlock (raft.py:33); scale = 1 gives raft_fs.CorrBlock's unnormalised products
  * (src/models/impls/raft_fs.py:13-87, whose pooled-feature dot equals the pooled volume).
- *   compute = RMD_F32  : exact f32 MFMA (v_mfma_f32_32x32x2_f32), the parity mode
- *   compute = RMD_BF16 : bf16 MFMA operands, f32 accumulation (performance mode)
+ *   compute = RMD_F32    : exact f32 MFMA (v_mfma_f32_32x32x2_f32)
+ *   compute = RMD_BF16X3 : fp32-accurate split bf16 MFMA, x = hi + lo, three bf16 products per
+ *                          k-step (~2^-16 relative per product; f32 storage, C <= 256; other cases
+ *                          run the exact f32 kernel) — the default parity mode
+ *   compute = RMD_BF16   : bf16 MFMA operands, f32 accumulation (performance mode)
  * All levels are produced by the GEMM epilogue from the f32 accumulators and stored as
  * desc->storage.
  */
@@ -91,8 +95,8 @@ int rmd_corr_pyramid(const float* fmap1, const float* fmap2, int channels, float
 
 /* Name of the GEMM kernel rmd_corr_pyramid runs for these arguments: "w8" (bf16 operands, fp16
  * pyramid, C <= 256: the performance path), "stationary" (the same with 64-bit store addressing, for
- * maps whose level-0 row span passes 1 GiB, e.g. 4K frames), "tiled" (exact f32 MFMA or any other
- * combination), or "invalid".  Host-only; for tests and introspection. */
+ * maps whose level-0 row span passes 1 GiB, e.g. 4K frames), "x3" (RMD_BF16X3 with an f32 pyramid),
+ * "tiled" (exact f32 MFMA or any other combination), or "invalid".  Host-only; for tests and introspection. */
 const char* rmd_corr_gemm_kernel(const rmd_pyramid_desc* desc, int channels, int compute);
 
 /* The two halves of rmd_corr_pyramid, for callers that time or overlap them separately:

@@ -21,6 +21,7 @@
 // Operands are first transposed to pixel-major, channel-contiguous (B, N, Cp) by prep_operand.
 
 #include "rmd_common.h"
+#include "corr_x3.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -1001,6 +1002,58 @@ __device__ __forceinline__ void mma(f32x16 (&acc)[8], bf16x8 (&bq)[16], const un
     mma_steps<0>(acc, bq, a, smem, lane_base, c, bnext);
 }
 
+// ---- padded, swizzle-free A layout (PAD = true) -------------------------------------------------
+// LDS row of block target (y, x) = (x>>3)*128 + y*8 + (x&7), rows 528 B apart (256 bf16 + 16 B pad).
+// The 32 targets of MFMA tile ti (4 rows x 8 cols) are then the consecutive LDS rows
+// (ti&1)*128 + (ti>>1)*32 + j, so lane (j, h)'s fragment of tile ti at k-step s sits at
+//   base[ti&1] + (ti>>1)*32*528 + 32*s,   base[e] = (e*128 + j)*528 + 16h:
+// two address VGPRs for the whole tile loop, everything else an instruction immediate (<= 51168).
+// Banks: 528 B = 33 x 16 B, so a ds_read_b128 lane group's 16 rows land in 16-B slots (row + chunk)
+// mod 16 = j mod 16 over lanes {0-3,12-15,20-27} and {4-11,16-19,28-31}: conflict-free, no XOR.
+constexpr unsigned kPadRow = 528;
+#ifndef RMD_W8_SCHED
+#define RMD_W8_SCHED 0
+#endif
+
+__device__ __forceinline__ int pad_row(int y, int x) { return ((x >> 3) << 7) + (y << 3) + (x & 7); }
+
+template <int S>
+__device__ __forceinline__ void mma_steps_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16], bf16x8 (&a)[8],
+                                              const unsigned char* smem, unsigned b0, unsigned b1) {
+    if constexpr (S < 16) {
+        const f32x16 zero = {};
+#pragma unroll
+        for (int ti = 0; ti < 8; ++ti) {
+            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ti], bq[S], S == 0 ? zero : acc[ti], 0, 0, 0);
+            // single-buffered: k-step S+1's fragment of tile ti replaces the one this MFMA consumed, so
+            // it has the 7 other MFMAs of the k-step (~224 cycles) to land
+            if constexpr (S + 1 < 16)
+                a[ti] = *reinterpret_cast<const bf16x8*>(smem + ((ti & 1) ? b1 : b0) +
+                                                         (unsigned)((ti >> 1) * 32 * kPadRow + 32 * (S + 1)));
+        }
+#if RMD_W8_SCHED == 1
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // 1 MFMA
+            if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // then 1 DS read
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#elif RMD_W8_SCHED == 2
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        mma_steps_pad<S + 1>(acc, bq, a, smem, b0, b1);
+    }
+}
+
+__device__ __forceinline__ void mma_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
+                                        unsigned b0, unsigned b1) {
+    bf16x8 a[8];
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti)
+        a[ti] = *reinterpret_cast<const bf16x8*>(smem + ((ti & 1) ? b1 : b0) + (unsigned)((ti >> 1) * 32 * kPadRow));
+    mma_steps_pad<0>(acc, bq, a, smem, b0, b1);
+}
+
 template <int S, int AUX>
 __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx& c, const pipe::LaneOff& lo,
                                          pipe::EpiState& st) {
@@ -1012,7 +1065,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx
 
 }  // namespace w8
 
-template <int AUX, bool ROLL>
+template <int AUX, bool ROLL, bool PAD = true>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
                 __half* __restrict__ pyr, int drop_stores, int stagger) {
@@ -1042,13 +1095,17 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
-        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
+        if constexpr (PAD)
+            *reinterpret_cast<uint4*>(smem + (size_t)w8::pad_row(row >> 4, row & 15) * w8::kPadRow + c * 16) = v;
+        else
+            *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
     }
     __syncthreads();
 
     const unsigned lane_row = 16u * (j >> 3) + (j & 7);
     const unsigned lane_base = lane_row * 512u;
     const unsigned lane_c = (unsigned)(h ^ a_swz((int)lane_row));
+    const unsigned pb0 = (unsigned)j * w8::kPadRow + 16u * h, pb1 = pb0 + 128u * w8::kPadRow;
 
     pipe::Ctx c;
 #pragma unroll
@@ -1105,7 +1162,13 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         // next tile's B fragments issue before this tile's stores, so waiting for them never
         // waits for the stores (vmcnt counts in issue order)
         const __bf16* pn = gB + (size_t)min(qn, nqt - 1) * 8192;
-        if constexpr (ROLL) {
+        if constexpr (PAD) {
+            unsigned b0 = pb0, b1 = pb1;
+            asm volatile("" : "+v"(b0), "+v"(b1));     // two opaque bases: every other offset is an immediate
+            w8::mma_pad(acc, bq, smem, b0, b1);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
+        } else if constexpr (ROLL) {
             w8::mma(acc, bq, smem, lane_base, lane_c, pn);
         } else {
             w8::mma(acc, bq, smem, lane_base, lane_c);
@@ -1124,10 +1187,11 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
 // store offsets (one wave's 16 level-0 rows < 1 GiB); larger maps (e.g. 4K frames) take the
 // stationary kernel (64-bit addressing), everything else the tiled kernel.  The diagnostic build
 // also honours RMD_GEMM_KERNEL = pipe | stationary | tiled.
-enum class Path { W8, PIPE, STATIONARY, TILED };
+enum class Path { W8, PIPE, STATIONARY, TILED, X3 };
 
 Path gemm_path(const rmd_pyramid_desc& d, int C, int compute) {
     const int Cp = (C + kKC - 1) / kKC * kKC;
+    if (compute == RMD_BF16X3) return x3::eligible(d, C) ? Path::X3 : Path::TILED;     // TILED: exact f32
     if (compute != RMD_BF16 || d.storage != RMD_F16 || Cp != 256) return Path::TILED;
 #ifdef RMD_DIAG
     const char* k_env = getenv("RMD_GEMM_KERNEL");
@@ -1192,18 +1256,24 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                 // pyramid is written once and read back a full GEMM later)
                 int qs = 1;
                 while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
-                auto kern = corr_pyramid_w8<2, false>;
+                auto kern = corr_pyramid_w8<2, false, true>;
+                int lds_w8 = 256 * (int)w8::kPadRow;
                 int drop = 0, stagger = 0;
 #ifdef RMD_DIAG
                 const int aux = env_knob("RMD_STORE_AUX", 2);
                 const bool roll = env_knob("RMD_W8_ROLL", 0) != 0;
-                kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true> : corr_pyramid_w8<2, false>)
-                                : (roll ? corr_pyramid_w8<0, true> : corr_pyramid_w8<0, false>);
+                if (env_knob("RMD_W8_PAD", 1) == 0) {      // previous XOR-swizzled layout
+                    kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true, false> : corr_pyramid_w8<2, false, false>)
+                                    : (roll ? corr_pyramid_w8<0, true, false> : corr_pyramid_w8<0, false, false>);
+                    lds_w8 = lds;
+                } else if (aux != 2) {
+                    kern = corr_pyramid_w8<0, false, true>;
+                }
                 drop = env_knob("RMD_ABLATE", 0) == 1;
                 stagger = env_knob("RMD_W8_STAGGER", 0);
 #endif
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                kern<<<nblk * d.batch * qs, 512, lds, st>>>(opA, opB, geom, qs, out, drop, stagger);
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds_w8);
+                kern<<<nblk * d.batch * qs, 512, lds_w8, st>>>(opA, opB, geom, qs, out, drop, stagger);
                 return check_launch("rmd_corr_pyramid/gemm-w8");
             }
 #ifdef RMD_DIAG
@@ -1245,7 +1315,8 @@ int check_args(const rmd_pyramid_desc* d, int channels, int compute) {
     RMD_REQUIRE(d, RMD_ERR_ARG, "rmd_corr_pyramid: null desc");
     RMD_REQUIRE(channels > 0, RMD_ERR_SHAPE, "rmd_corr_pyramid: channels must be > 0");
     RMD_REQUIRE(d->levels >= 1 && d->levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_pyramid: bad levels");
-    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16, RMD_ERR_ARG, "rmd_corr_pyramid: compute must be F32 or BF16");
+    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16 || compute == RMD_BF16X3, RMD_ERR_ARG,
+                "rmd_corr_pyramid: compute must be F32, BF16 or BF16X3");
     RMD_REQUIRE(d->storage == RMD_F32 || d->storage == RMD_F16, RMD_ERR_ARG, "rmd_corr_pyramid: storage must be F32 or F16");
     return RMD_OK;
 }
@@ -1255,6 +1326,10 @@ int check_args(const rmd_pyramid_desc* d, int channels, int compute) {
 
 extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, int channels, int compute) {
     if (!d || channels <= 0) return 0;
+    if (compute == RMD_BF16X3) {
+        if (rmd::x3::eligible(*d, channels)) return rmd::x3::workspace_bytes(*d);
+        compute = RMD_F32;
+    }
     const size_t Cp = (size_t)(channels + rmd::kKC - 1) / rmd::kKC * rmd::kKC;
     const size_t es = compute == RMD_F32 ? 4 : 2;
     const size_t N = (size_t)d->height * d->width, Npad = (N + 31) / 32 * 32;   // B operand padded to 32-query tiles
@@ -1267,6 +1342,7 @@ extern "C" const char* rmd_corr_gemm_kernel(const rmd_pyramid_desc* d, int chann
         case rmd::Path::W8: return "w8";
         case rmd::Path::PIPE: return "pipe";
         case rmd::Path::STATIONARY: return "stationary";
+        case rmd::Path::X3: return "x3";
         default: return "tiled";
     }
 }
@@ -1277,6 +1353,11 @@ extern "C" int rmd_corr_prepare(const float* fmap1, const float* fmap2, int chan
     int rc = rmd::check_args(d, channels, compute);
     if (rc) return rc;
     hipStream_t st = rmd::as_stream(stream);
+    if (compute == RMD_BF16X3) {
+        if (rmd::gemm_path(*d, channels, compute) == rmd::Path::X3)
+            return rmd::x3::prepare(fmap1, fmap2, channels, scale, *d, workspace, st);
+        compute = RMD_F32;
+    }
     return compute == RMD_BF16 ? rmd::launch_prepare<false>(fmap1, fmap2, channels, scale, *d, workspace, st)
                                : rmd::launch_prepare<true>(fmap1, fmap2, channels, scale, *d, workspace, st);
 }
@@ -1287,6 +1368,10 @@ extern "C" int rmd_corr_pyramid_prepared(int channels, float scale, const rmd_py
     int rc = rmd::check_args(d, channels, compute);
     if (rc) return rc;
     hipStream_t st = rmd::as_stream(stream);
+    if (compute == RMD_BF16X3) {
+        if (rmd::gemm_path(*d, channels, compute) == rmd::Path::X3) return rmd::x3::pyramid(*d, pyramid, workspace, st);
+        compute = RMD_F32;
+    }
     if (compute == RMD_BF16)
         return d->storage == RMD_F16 ? rmd::launch_pyramid<false, __half>(channels, scale, *d, pyramid, workspace, st)
                                      : rmd::launch_pyramid<false, float>(channels, scale, *d, pyramid, workspace, st);

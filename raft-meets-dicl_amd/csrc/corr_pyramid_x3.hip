@@ -1,0 +1,398 @@
+// corr_pyramid_x3.hip — fp32-accurate correlation GEMM + fused pooled pyramid from split-bf16 MFMAs.
+//
+// Replaces raft.CorrBlock.__init__ (qzed/raft-meets-dicl src/models/impls/raft.py:18-47) in the
+// fp32 parity mode.  The reference computes the volume in fp32 (raft.py:31-33, fmaps .float() at
+// :381); exact f32 MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate, so each operand is
+// split x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (16 significant bits together) and
+//   corr = A_hi.B_hi + A_hi.B_lo + A_lo.B_hi        (the dropped lo.lo term is ~2^-16 relative)
+// runs as three v_mfma_f32_32x32x16_bf16 per k-step into one fp32 accumulator: 3/16 of the exact-
+// f32 MFMA cost.  The 1/sqrt(C) scale is folded into fmap2 before the split (fp32 multiply).
+//
+// Geometry: one workgroup (8 waves, two per SIMD) owns an 8 x 16 block of target
+// pixels — both split halves of its A operand sit in LDS as one 1072-B row per target (hi 512 B,
+// lo 512 B, 48 B pad; 1072 = 67 x 16 B, so a ds_read_b128 lane group's 16 consecutive rows hit 16
+// distinct 16-B bank slots, see w8::pad_row in corr_pyramid.hip) — and each wave sweeps its own
+// 32-query tiles: 4 MFMA tiles (4 x 8 targets each) x 16 k-steps x 3 products = 192 MFMAs, then
+// pools in-lane and stores all four fp32 levels straight from the accumulators with range-checked
+// buffer stores (rows past the level fall outside the descriptor, chunks past the row get a 1 GiB
+// bias).  fp32 level-0 chunks are 32 B per query, so lane h of a query writes bytes 16h..16h+15 and
+// every level-0 store instruction is one contiguous 1 KiB run without a lane exchange.
+
+#include "rmd_common.h"
+#include "corr_x3.h"
+
+namespace rmd {
+namespace x3 {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+
+constexpr int kRow = 1072;                  // LDS bytes per target row: hi 512 + lo 512 + 48 pad
+constexpr int kBlockRows = 8, kBlockCols = 16;
+constexpr unsigned kBig = 0x40000000u;      // offset bias beyond every level's range
+
+// LDS row of block target (y 0..7, x 0..15): tile (rg = y>>2, cg = x>>3) holds rows
+// cg*64 + rg*32 + (y&3)*8 + (x&7), i.e. lane j of an MFMA tile reads row base + j.
+__device__ __forceinline__ int lds_row(int y, int x) { return ((x >> 3) << 6) + (y << 3) + (x & 7); }
+
+__device__ __forceinline__ __bf16 hi_part(float v) { return (__bf16)v; }
+__device__ __forceinline__ __bf16 lo_part(float v) { return (__bf16)(v - (float)(__bf16)v); }
+
+// ---- operand prep: both feature maps, split, in one launch ------------------------------------
+// grid (128-pixel tiles, B, 2).  z = 0: fmap2 * scale -> A hi / lo, pixel-major (B, N, 256);
+// z = 1: fmap1 -> B hi / lo in MFMA B-fragment order o[b][qt][s][lane][8] (lane = j + 32h: channels
+// 16s + 8h .. +7 of query min(32 qt + j, N - 1)).  Read phase as prep_pair (float4 per channel row),
+// hi and lo tiles staged in LDS, one 16-B chunk per lane-store on the write side.
+constexpr int kPx = 128, kStride = 256 * 2 + 16;
+
+__global__ void __launch_bounds__(512)
+prep_split(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* __restrict__ aHi,
+           __bf16* __restrict__ aLo, __bf16* __restrict__ bHi, __bf16* __restrict__ bLo, int C, int N, int nqt,
+           float scale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* tHi = lds;
+    unsigned char* tLo = lds + kPx * kStride;
+    const int b = blockIdx.y, which = blockIdx.z;
+    const float* f = which ? f1 : f2;
+    const float s = which ? 1.0f : scale;
+    const int t = threadIdx.x;
+    const int p0 = blockIdx.x * kPx;
+    const bool full = p0 + kPx <= N && (N & 3) == 0;
+    const int pl = N - 1 - p0;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int item = it * 512 + t;               // (channel octet cg, pixel quad q), q fastest
+        const int q = item & 31, cg = item >> 5;
+        float v[8][4];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = cg * 8 + e;
+            const float* src = f + ((size_t)b * C + c) * N + p0 + 4 * q;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c < C) {
+                if (full) {
+                    x = *reinterpret_cast<const float4*>(src);
+                } else {
+                    x.x = src[min(4 * q + 0, pl) - 4 * q];
+                    x.y = src[min(4 * q + 1, pl) - 4 * q];
+                    x.z = src[min(4 * q + 2, pl) - 4 * q];
+                    x.w = src[min(4 * q + 3, pl) - 4 * q];
+                }
+            }
+            v[e][0] = x.x * s;
+            v[e][1] = x.y * s;
+            v[e][2] = x.z * s;
+            v[e][3] = x.w * s;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            bf16x8 hi, lo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                hi[e] = hi_part(v[e][i]);
+                lo[e] = lo_part(v[e][i]);
+            }
+            *reinterpret_cast<bf16x8*>(tHi + (size_t)(4 * q + i) * kStride + cg * 16) = hi;
+            *reinterpret_cast<bf16x8*>(tLo + (size_t)(4 * q + i) * kStride + cg * 16) = lo;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int k = it * 512 + t;                  // 16-B output chunk of the tile's 64 KiB block
+        int px, c0;
+        if (which) {
+            const int L = k & 63, st = (k >> 6) & 15;
+            px = (k >> 10) * 32 + (L & 31);
+            c0 = 16 * st + 8 * (L >> 5);
+        } else {
+            px = k >> 5;
+            c0 = (k & 31) * 8;
+        }
+        const bf16x8 hi = *reinterpret_cast<const bf16x8*>(tHi + (size_t)px * kStride + c0 * 2);
+        const bf16x8 lo = *reinterpret_cast<const bf16x8*>(tLo + (size_t)px * kStride + c0 * 2);
+        if (which) {
+            const int qt = blockIdx.x * 4 + (k >> 10);
+            if (qt < nqt) {
+                const size_t o = (((size_t)b * nqt + qt) * 1024 + (k & 1023)) * 8;
+                *reinterpret_cast<bf16x8*>(bHi + o) = hi;
+                *reinterpret_cast<bf16x8*>(bLo + o) = lo;
+            }
+        } else if (p0 + px < N) {
+            const size_t o = ((size_t)b * N + p0) * 256 + (size_t)k * 8;
+            *reinterpret_cast<bf16x8*>(aHi + o) = hi;
+            *reinterpret_cast<bf16x8*>(aLo + o) = lo;
+        }
+    }
+}
+
+// ---- store descriptors -------------------------------------------------------------------------
+struct Lvl {
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned rs;      // row stride (bytes)
+    unsigned cs;      // chunk stride (bytes)
+    int rows;         // valid rows of this block on the level
+    int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
+};
+
+__device__ __forceinline__ unsigned soff(const Lvl& L, int row, int chunk) {
+    return (row < L.rows && chunk < L.chunks) ? (unsigned)row * L.rs + (unsigned)chunk * L.cs : kBig;
+}
+
+__device__ __forceinline__ void swap32(unsigned& x, unsigned& y) {
+    auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+
+__device__ __forceinline__ void swapf(float& x, float& y) {
+    unsigned a = __float_as_uint(x), b = __float_as_uint(y);
+    swap32(a, b);
+    x = __uint_as_float(a);
+    y = __uint_as_float(b);
+}
+
+constexpr int AUX_NT = 2;     // non-temporal stores: the pyramid is re-read a whole GEMM later
+
+// Epilogue of one 32-query tile: acc[ti] (ti = 2 rg + cg) holds, for lane (j, h), the targets
+// (row 4 rg + k, col 8 cg + 4 h + e) at acc[ti][4k + e].
+__device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[4], int q, int h) {
+    const unsigned qo[4] = {(unsigned)q * 32u + 16u * h, (unsigned)q * 32u + 16u * h, (unsigned)q * 16u + 8u * h,
+                            (unsigned)q * 8u + 4u * h};
+    // level 0: 16 stores of 16 B (row 4rg + k, chunk cg, bytes 16h..)
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const i32x4 d = {__float_as_int(acc[ti][4 * k + 0]), __float_as_int(acc[ti][4 * k + 1]),
+                             __float_as_int(acc[ti][4 * k + 2]), __float_as_int(acc[ti][4 * k + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(d, L[0].rsrc, (int)(qo[0] + soff(L[0], 4 * (ti >> 1) + k, ti & 1)),
+                                                   0, AUX_NT);
+        }
+    // level 1: tile rows (2m, 2m+1) -> level-1 row 2rg + m; lane pair u -> block col 4cg + 2h + u
+    float s2[2][2];      // level-2 sums [rg][cg] (16 level-0 values each)
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            float p[2][2];       // [cg][u]
+#pragma unroll
+            for (int cg = 0; cg < 2; ++cg)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const f32x16& a = acc[2 * rg + cg];
+                    p[cg][u] = (a[4 * (2 * m) + 2 * u] + a[4 * (2 * m) + 2 * u + 1]) +
+                               (a[4 * (2 * m + 1) + 2 * u] + a[4 * (2 * m + 1) + 2 * u + 1]);
+                }
+#pragma unroll
+            for (int cg = 0; cg < 2; ++cg) {
+                const float t = p[cg][0] + p[cg][1];
+                s2[rg][cg] = m == 0 ? t : s2[rg][cg] + t;
+            }
+            // lower lanes keep cols {0,1} and receive {2,3}; upper lanes receive {4,5}, keep {6,7}
+            float x0 = p[0][0], x1 = p[0][1], y0 = p[1][0], y1 = p[1][1];
+            swapf(x0, y0);
+            swapf(x1, y1);
+            const i32x4 d = {__float_as_int(0.25f * x0), __float_as_int(0.25f * x1), __float_as_int(0.25f * y0),
+                             __float_as_int(0.25f * y1)};
+            __builtin_amdgcn_raw_buffer_store_b128(d, L[1].rsrc, (int)(qo[1] + soff(L[1], 2 * rg + m, 0)), 0, AUX_NT);
+        }
+    }
+    // level 2: row rg, lane holds col h (cg 0) and 2 + h (cg 1); after the swap lower = {0,1}, upper = {2,3}
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg) {
+        float x = s2[rg][0], y = s2[rg][1];
+        swapf(x, y);
+        const i32x2 d = {__float_as_int(0.0625f * x), __float_as_int(0.0625f * y)};
+        __builtin_amdgcn_raw_buffer_store_b64(d, L[2].rsrc, (int)(qo[2] + soff(L[2], rg, 0)), 0, AUX_NT);
+    }
+    // level 3: one row, col cg = both tile rows and both lane halves of column group cg
+    {
+        float x = s2[0][0] + s2[1][0], y = s2[0][1] + s2[1][1];
+        swapf(x, y);         // lower: own + upper's col-0 partial; upper: lower's + own col-1 partial
+        const float v = (1.0f / 64.0f) * (x + y);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), L[3].rsrc, (int)(qo[3] + soff(L[3], 0, 0)), 0,
+                                              AUX_NT);
+    }
+}
+
+constexpr int kRing = 4;     // B ring slots (16 % kRing == 0: k-step s of every tile maps to slot s % kRing)
+
+// A fragments (hi in [2ti], lo in [2ti+1]) of k-step S for the 4 target tiles
+template <int S>
+__device__ __forceinline__ void read_a(bf16x8 (&a)[8], const unsigned char* smem, unsigned b0, unsigned b1) {
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+        const unsigned base = ((ti & 1) ? b1 : b0) + (unsigned)((ti >> 1) * 32 * kRow + 32 * S);
+        a[2 * ti] = *reinterpret_cast<const bf16x8*>(smem + base);
+        a[2 * ti + 1] = *reinterpret_cast<const bf16x8*>(smem + base + 512);
+    }
+}
+
+template <int S>
+__device__ __forceinline__ void ksteps(f32x16 (&acc)[4], bf16x8 (&acur)[8], bf16x8 (&anext)[8], bf16x8 (&rh)[kRing],
+                                       bf16x8 (&rl)[kRing], const unsigned char* smem, unsigned b0, unsigned b1,
+                                       const __bf16* curH, const __bf16* curL, const __bf16* nxtH,
+                                       const __bf16* nxtL) {
+    if constexpr (S < 16) {
+        if constexpr (S + 1 < 16) read_a<S + 1>(anext, smem, b0, b1);
+        {   // B fragment of k-step S + kRing - 1 (this tile) or of the next tile's k-step S + kRing - 1 - 16
+            constexpr int T = S + kRing - 1, slot = T % kRing;
+            const __bf16* ph = T < 16 ? curH : nxtH;
+            const __bf16* pl = T < 16 ? curL : nxtL;
+            rh[slot] = *reinterpret_cast<const bf16x8*>(ph + 512 * (T & 15));
+            rl[slot] = *reinterpret_cast<const bf16x8*>(pl + 512 * (T & 15));
+        }
+        const f32x16 zero = {};
+        const bf16x8 bh = rh[S % kRing], bl = rl[S % kRing];
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti) {
+            f32x16 c = S == 0 ? zero : acc[ti];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti + 1], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bl, c, 0, 0, 0);
+            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bh, c, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);      // one scheduling region per k-step
+        ksteps<S + 1>(acc, anext, acur, rh, rl, smem, b0, b1, curH, curL, nxtH, nxtL);
+    }
+}
+
+__global__ void __launch_bounds__(512, 1)
+corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
+                const __bf16* __restrict__ bLo, PyrGeom g, int qsplit, float* __restrict__ pyr) {
+    constexpr int WAVES = 8;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = g.height, W = g.width, N = H * W;
+    const int ncb = (W + kBlockCols - 1) / kBlockCols;
+    const int nblk = ((H + kBlockRows - 1) / kBlockRows) * ncb;
+    const int lid = xcd_block(blockIdx.x, gridDim.x);
+    const int tb = lid % nblk;
+    const int rest = lid / nblk;
+    const int split_ = rest % qsplit;
+    const int b = rest / qsplit;
+    const int rb = tb / ncb, cb = tb - rb * ncb;
+    const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+
+    // ---- A block (hi and lo) -> LDS, zero rows for targets outside the image --------------------
+    const size_t abase = (size_t)b * N * 256;
+    for (int id = tid; id < kBlockRows * kBlockCols * 64; id += 64 * WAVES) {
+        const int row = id >> 6, c = id & 63;                 // c < 32: hi chunk c, else lo chunk c - 32
+        const int y = row >> 4, x = row & 15;
+        const int ty = ty0 + y, tx = tx0 + x;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        const __bf16* src = c < 32 ? aHi : aLo;
+        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
+        *reinterpret_cast<uint4*>(smem + (size_t)lds_row(y, x) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v;
+    }
+    __syncthreads();
+
+    // ---- per-level store descriptors of this block (wave-uniform) -------------------------------
+    Lvl L[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int span = kBlockRows >> l, nch = l == 0 ? 2 : 1;
+        const int y0 = rb * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        const int cw = g.tw[l];
+        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 4u : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
+        float* bp = pyr + base;
+        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+        L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+                                                      (int)__builtin_amdgcn_readfirstlane((unsigned)rows * rs), 0x00020000);
+        L[l].rs = __builtin_amdgcn_readfirstlane(rs);
+        L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
+        L[l].rows = __builtin_amdgcn_readfirstlane(rows);
+        L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+    }
+
+    // A fragment of tile ti = 2 rg + cg, k-step s, half p: base[cg] + rg*32*kRow + 32 s + 512 p
+    unsigned b0 = (unsigned)j * kRow + 16u * h, b1 = b0 + 64u * kRow;
+    asm volatile("" : "+v"(b0), "+v"(b1));
+
+    const int nqt = (N + 31) >> 5;
+    const size_t bb = ((size_t)b * nqt * 1024 + lane) * 8;
+    const int stride = WAVES * qsplit;
+    int qt = split_ * WAVES + w;
+    if (qt >= nqt) return;
+    // B fragments stream through a 4-slot register ring: k-step s of a tile lives in slot s % 4 and is
+    // loaded at k-step s - 3 (the previous tile's k-steps 13-15 load this tile's 0-2), ~3 k-steps
+    // (36 MFMAs) ahead; A fragments of k-step s + 1 are read from LDS at the top of k-step s.  Each
+    // k-step is one scheduling region, so neither set of loads drifts to just before its MFMAs.
+    const __bf16* pb = bHi + bb + (size_t)qt * 8192;
+    const __bf16* pbl = bLo + bb + (size_t)qt * 8192;
+    bf16x8 rh[kRing], rl[kRing];
+#pragma unroll
+    for (int s = 0; s < kRing - 1; ++s) {
+        rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
+        rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
+    }
+    while (true) {
+        f32x16 acc[4];
+        const int qn = qt + stride;
+        const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+        bf16x8 a0[8], a1[8];
+        read_a<0>(a0, smem, b0, b1);
+        ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192, bLo + bb + (size_t)qt * 8192,
+                  bHi + bb + pn, bLo + bb + pn);
+        epilogue(acc, L, min(qt * 32 + j, N - 1), h);
+        if (qn >= nqt) break;
+        qt = qn;
+    }
+}
+
+}  // namespace
+
+bool eligible(const rmd_pyramid_desc& d, int C) {
+    if (C > 256 || d.storage != RMD_F32 || d.levels < 1) return false;
+    // every block's per-level store range (rows x row stride, bytes) plus the 1 GiB chunk bias must
+    // stay inside 32-bit buffer offsets
+    const double N = (double)d.height * d.width;
+    const double span0 = 8.0 * d.tiles_x[0] * N * 8 * 4;
+    return span0 < (double)(1u << 30);
+}
+
+size_t workspace_bytes(const rmd_pyramid_desc& d) {
+    const size_t N = (size_t)d.height * d.width, Npad = (N + 31) / 32 * 32;
+    return (size_t)d.batch * (N + Npad) * 256 * 2 * 2;
+}
+
+int prepare(const float* f1, const float* f2, int C, float scale, const rmd_pyramid_desc& d, void* ws,
+            hipStream_t st) {
+    const int N = d.height * d.width, nqt = (N + 31) / 32;
+    __bf16* aHi = reinterpret_cast<__bf16*>(ws);
+    __bf16* aLo = aHi + (size_t)d.batch * N * 256;
+    __bf16* bHi = aLo + (size_t)d.batch * N * 256;
+    __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
+    const int lds = 2 * kPx * kStride;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prep_split), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    prep_split<<<dim3((N + kPx - 1) / kPx, d.batch, 2), 512, lds, st>>>(f1, f2, aHi, aLo, bHi, bLo, C, N, nqt, scale);
+    return check_launch("rmd_corr_prepare/x3");
+}
+
+int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
+    const int N = d.height * d.width, nqt = (N + 31) / 32;
+    const __bf16* aHi = reinterpret_cast<const __bf16*>(ws);
+    const __bf16* aLo = aHi + (size_t)d.batch * N * 256;
+    const __bf16* bHi = aLo + (size_t)d.batch * N * 256;
+    const __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
+    const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
+    int qs = 1;
+    while (nblk * d.batch * qs < 256 && qs * 16 <= nqt) qs *= 2;
+    const int lds = kBlockRows * kBlockCols * kRow;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_x3), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    corr_pyramid_x3<<<nblk * d.batch * qs, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), qs,
+                                                           reinterpret_cast<float*>(pyr));
+    return check_launch("rmd_corr_pyramid/gemm-x3");
+}
+
+}  // namespace x3
+}  // namespace rmd

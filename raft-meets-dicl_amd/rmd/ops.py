@@ -9,11 +9,12 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import RMD_BF16, RMD_F16, RMD_F32
+from ._lib import RMD_BF16, RMD_BF16X3, RMD_F16, RMD_F32
 
 # precision modes: (GEMM compute type, pyramid storage type)
 PRECISIONS = {
-    "fp32": (RMD_F32, RMD_F32),       # exact f32 MFMA, f32 pyramid: the parity mode (default)
+    "fp32": (RMD_BF16X3, RMD_F32),    # fp32-accurate split-bf16 MFMA (3 products), f32 pyramid: parity mode (default)
+    "fp32-exact": (RMD_F32, RMD_F32), # exact f32 MFMA (v_mfma_f32_32x32x2_f32), f32 pyramid
     "bf16": (RMD_BF16, RMD_F16),      # bf16 MFMA operands, f32 accumulate, fp16 pyramid: perf mode
     "bf16-f32": (RMD_BF16, RMD_F32),  # bf16 operands, f32 pyramid
     "fp32-f16": (RMD_F32, RMD_F16),   # exact f32 GEMM, fp16 pyramid
@@ -143,6 +144,8 @@ def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
     compute = PRECISIONS[precision or _default_precision][0]
+    if compute == RMD_BF16X3:           # the on-the-fly kernels take exact f32 or bf16 operands
+        compute = RMD_F32
     f1 = fmap1.detach().float().contiguous()
     f2 = fmap2.detach().float().contiguous()
     b, c, h, w = f1.shape

@@ -5,7 +5,8 @@ float64 CPU oracle at the same seeded inputs, and (3) at the full cfg2 size (B=8
 against the oracle on a random sample of queries plus determinism.
 
 Tolerances (max|got-ref| / max|ref|, conftest.rel_max_err):
-  * fp32 mode (exact f32 MFMA, f32 pyramid): 1e-4 — north_star's cost-volume gate
+  * fp32 mode (split-bf16 MFMA hi.hi + hi.lo + lo.hi, f32 pyramid) and fp32-exact (exact f32 MFMA):
+    1e-4 — north_star's cost-volume gate
   * bf16 mode (bf16 operands, f32 accumulation, fp16 pyramid): 1e-2 — operand rounding 2^-9
 """
 
@@ -18,7 +19,7 @@ from conftest import load_golden, rel_max_err
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": 1e-4, "bf16": 1e-2, "bf16-f32": 1e-2, "fp32-f16": 2e-3}
+TOL = {"fp32": 1e-4, "fp32-exact": 1e-4, "bf16": 1e-2, "bf16-f32": 1e-2, "fp32-f16": 2e-3}
 CORR_CASES = ["corr_b2_c32_24x40", "corr_b2_c32_24x40_mask", "corr_b1_c256_16x24_pyr",
               "corr_b1_c16_12x20_nan", "corr_b1_c32_20x28_r7_l2", "corr_b2_c64_17x23_l1"]
 DEV = "cuda"
@@ -28,7 +29,7 @@ def _t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16-f32", "fp32-f16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16"])
 @pytest.mark.parametrize("name", CORR_CASES)
 def test_corr_block_matches_reference_golden(name, precision):
     import rmd
@@ -42,13 +43,14 @@ def test_corr_block_matches_reference_golden(name, precision):
     assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
 
 
-def test_pyramid_levels_match_reference_golden():
+@pytest.mark.parametrize("precision,tol", [("fp32-exact", 1e-5), ("fp32", 1e-4)])
+def test_pyramid_levels_match_reference_golden(precision, tol):
     import rmd
     g = load_golden("corr_b1_c256_16x24_pyr")
-    cb = rmd.raft.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), 4, 4, precision="fp32")
+    cb = rmd.raft.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), 4, 4, precision=precision)
     for i, lvl in enumerate(cb.corr_pyramid):
         assert tuple(lvl.shape) == g[f"pyr{i}"].shape
-        assert rel_max_err(lvl.cpu().numpy(), g[f"pyr{i}"]) < 1e-5
+        assert rel_max_err(lvl.cpu().numpy(), g[f"pyr{i}"]) < tol
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -150,9 +152,12 @@ def test_stationary_path_4k_sampled_vs_oracle():
 
 
 def test_gemm_kernel_routing():
-    """cfg2 bf16 -> w8, fp32 -> tiled (exact f32 MFMA), 4K bf16 -> stationary."""
+    """cfg2 bf16 -> w8, fp32 -> x3 (split bf16), fp32-exact -> tiled (exact f32 MFMA), 4K bf16 -> stationary."""
     from rmd import _lib
     lib = _lib.lib()
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F32), 256, _lib.RMD_BF16X3) == b"x3"
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F32), 320, _lib.RMD_BF16X3) == b"tiled"
+    assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F16), 256, _lib.RMD_BF16X3) == b"tiled"
     assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F16), 256, _lib.RMD_BF16) == b"w8"
     assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F32), 256, _lib.RMD_F32) == b"tiled"
     assert lib.rmd_corr_gemm_kernel(_lib.describe(8, 55, 128, 4, _lib.RMD_F16), 128, _lib.RMD_BF16) == b"tiled"

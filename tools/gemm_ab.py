@@ -11,6 +11,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the A/B knobs exist only in the diagnostic build (make -C raft-meets-dicl_amd/csrc diag)
+os.environ.setdefault("RMD_LIBRARY", os.path.join(ROOT, "raft-meets-dicl_amd", "rmd", "librmd_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
@@ -33,6 +35,7 @@ def main():
         kern, _, aux = kern.partition("@")          # e.g. "w8@2" = RMD_STORE_AUX=2
         kern, _, knobs = kern.partition("+")        # e.g. "w8+roll+stag4" = RMD_W8_ROLL=1, RMD_W8_STAGGER=4
         os.environ["RMD_W8_ROLL"] = "1" if "roll" in knobs else "0"
+        os.environ["RMD_W8_PAD"] = "0" if "nopad" in knobs else "1"      # "w8+nopad" = XOR-swizzled LDS
         stag = int(knobs.split("stag")[1].split("+")[0]) if "stag" in knobs else 0
         os.environ["RMD_W8_STAGGER"] = str(stag + (1000 if "prio" in knobs else 0))     # "w8+prio" = s_setprio 1 on waves 4-7
         os.environ["RMD_GEMM_KERNEL"] = kern
