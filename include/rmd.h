@@ -136,11 +136,12 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * Backward of the RAFT correlation (training; autograd of raft.py:18-95).  Coordinates are
  * detached in the reference (raft.py:402), so only the feature maps receive gradients.
  *
- * Gradient of the pyramid, dense float32 "G": (B, N, T) row-major with T = rmd_corr_grad_targets()
- * = sum_l H_l*W_l; level l of query row (b, p) occupies columns [t_off(l), t_off(l) + H_l*W_l) with
- * t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at t_off(l) + y*W_l + x.  With
- * P = rmd_corr_pool_targets(fmap2, scale = 1/sqrt(C)) as (B, T, C):
- *   grad_fmap1 (B, C, N) = P^T G^T    and    dP (B, T, C) = G^T fmap1^T      (plain GEMMs)
+ * Gradient of the pyramid, dense float32 "G": (B, T, N) row-major, query-minor (the forward
+ * pyramid's orientation), T = rmd_corr_grad_targets() = sum_l H_l*W_l; level l occupies rows
+ * [t_off(l), t_off(l) + H_l*W_l) with t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at row
+ * t_off(l) + y*W_l + x, query p in column p.  With P = rmd_corr_pool_targets(fmap2, scale =
+ * 1/sqrt(C)) as (B, T, C):
+ *   grad_fmap1 (B, C, N) = P^T G    and    dP (B, T, C) = G fmap1^T      (plain GEMMs)
  *   grad_fmap2 = rmd_corr_unpool_targets(dP, scale = 1/sqrt(C)).
  */
 

@@ -11,13 +11,17 @@
 //     dfmap1[p]  = sum_l sum_t G_l[p, t] P_l[t]                         (GEMM, K = sum_l T_l)
 //     dP_l[t]    = sum_p G_l[p, t] fmap1[p]                              (GEMM, K = N)
 //     dfmap2     = sum_l unpool_l(dP_l) / sqrt(C)                        (this file)
-//   G (all levels, all lookups of a forward) is accumulated densely as (B, N, T) float32,
-//   T = sum_l H_l W_l, level l's targets at column offset t_off[l] = sum_{l'<l} H_l' W_l', row-major
-//   (y, x) inside a level — a plain strided matrix, so both GEMMs are library GEMMs.
-//   rmd_corr_lookup_backward: one lane per (query, level) owns row (b, p) of level l: it spreads
-//   the (2r+1)^2 tap gradients over its (2r+2)^2 integer patch with the forward's bilinear
-//   weights (separable: x then y) and read-modify-writes the patch — no atomics, no other lane
-//   touches that row in the launch, and successive lookups are ordered by the stream.
+//   G (all levels, all lookups of a forward) is accumulated densely as (B, T, N) float32, query-minor
+//   like the forward pyramid: T = sum_l H_l W_l, level l's targets at row offset
+//   t_off[l] = sum_{l'<l} H_l' W_l', row-major (y, x) inside a level — a plain matrix, so both GEMMs
+//   are library GEMMs without transposes (dfmap1 = P^T G lands directly in (B, C, N)).
+//   rmd_corr_lookup_backward: lanes are consecutive queries, so a lane group whose (smooth) flow puts
+//   their patches on the same target row-column touches one contiguous 256-B run of G per access
+//   (the (B, N, T) layout made every wave access 64 different rows).  Each lane owns column (b, p)
+//   of G for its level: it spreads the (2r+1)^2 tap gradients over its (2r+2)^2 integer patch with
+//   the forward's bilinear weights (separable: x then y) and read-modify-writes the patch — no
+//   atomics: the patch rows are split over 3 lanes (parts) that write disjoint rows, no other lane
+//   touches column p, and successive lookups are ordered by the stream.
 
 #include "rmd_common.h"
 
@@ -52,15 +56,19 @@ inline GradGeom make_grad_geom(int batch, int h, int w, int levels) {
     return g;
 }
 
-// grid: (query blocks, batch, level); one lane per (query, level)
+// grid: (query blocks of 64, batch, level + levels * part); one lane per (query, level, part), part k
+// producing patch rows [k*PR, min(K, (k+1)*PR)) from tap rows k*PR - 1 .. (k+1)*PR - 1
+constexpr int kBwdThreads = 64, kBwdParts = 3;
+
 template <int R>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kBwdThreads)
 corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const float* __restrict__ coords,
                             unsigned zmask, float* __restrict__ grad) {
-    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, PR = (K + kBwdParts - 1) / kBwdParts;
     const int N = g.height * g.width;
-    const int p = blockIdx.x * kThreads + threadIdx.x;
-    const int b = blockIdx.y, L = blockIdx.z;
+    const int p = blockIdx.x * kBwdThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    const int L = (int)blockIdx.z % g.levels, part = (int)blockIdx.z / g.levels;
     if (p >= N) return;
     if ((zmask >> L) & 1u) return;                       // zeroed level (raft.py:86-87): no gradient
     const int lh = g.lh[L], lw = g.lw[L];
@@ -75,34 +83,38 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
     const int xs = (int)fx0 - R, ys = (int)fy0 - R;
 
     const float* go = gout + ((size_t)b * g.levels + L) * D * D * (size_t)N + p;
-    float* row = grad + ((size_t)b * N + p) * g.T + g.toff[L];
+    float* col = grad + ((size_t)b * g.T + g.toff[L]) * (size_t)N + p;      // G[b][t_off + y*lw + x][p]
 
-    // x pass per tap row bb: Q[bb][i] = g[i][bb](1-fx) + g[i-1][bb] fx, i = 0..K-1
-    // y pass: P[j][i] = Q[j][i](1-fy) + Q[j-1][i] fy; rows j of the patch are written as produced
-    float qprev[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) qprev[i] = 0.f;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        float qcur[K];
-        if (j < D) {
+    // x pass of tap row j: Q[j][i] = g[i][j](1-fx) + g[i-1][j] fx, i = 0..K-1 (zero for j outside 0..D-1)
+    auto qrow = [&](int j, float (&q)[K]) {
+        if (j >= 0 && j < D) {
             float gr[D];
 #pragma unroll
-            for (int a = 0; a < D; ++a) gr[a] = go[(size_t)(a * D + j) * N];   // channel a*D + bb, bb = j
+            for (int a = 0; a < D; ++a) gr[a] = go[(size_t)(a * D + j) * N];   // channel a*D + j
 #pragma unroll
-            for (int i = 0; i < K; ++i)
-                qcur[i] = (i < D ? gr[i] * (1.0f - fx) : 0.f) + (i >= 1 ? gr[i - 1] * fx : 0.f);
+            for (int i = 0; i < K; ++i) q[i] = (i < D ? gr[i] * (1.0f - fx) : 0.f) + (i >= 1 ? gr[i - 1] * fx : 0.f);
         } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) qcur[i] = 0.f;
+            for (int i = 0; i < K; ++i) q[i] = 0.f;
         }
+    };
+    // y pass: patch row j = Q[j](1-fy) + Q[j-1] fy
+    const int j0 = part * PR, j1 = min(K, j0 + PR);
+    float qprev[K];
+    qrow(j0 - 1, qprev);
+#pragma unroll
+    for (int jj = 0; jj < PR; ++jj) {
+        const int j = j0 + jj;
+        if (j >= j1) break;
+        float qcur[K];
+        qrow(j, qcur);
         const int y = ys + j;
         if (y >= 0 && y < lh) {
-            float* r = row + (size_t)y * lw;
+            float* r = col + (size_t)y * lw * N;
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 const int x = xs + i;
-                if (x >= 0 && x < lw) r[x] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                if (x >= 0 && x < lw) r[(size_t)x * N] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
             }
         }
 #pragma unroll
@@ -182,11 +194,11 @@ extern "C" int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(d->batch, d->height, d->width, d->levels);
     const int N = d->height * d->width;
-    dim3 grid((N + rmd::kThreads - 1) / rmd::kThreads, d->batch, d->levels);
+    dim3 grid((N + rmd::kBwdThreads - 1) / rmd::kBwdThreads, d->batch, d->levels * rmd::kBwdParts);
     hipStream_t st = rmd::as_stream(stream);
     switch (radius) {
 #define RMD_CASE(RR) \
-    case RR: rmd::corr_lookup_backward_kernel<RR><<<grid, rmd::kThreads, 0, st>>>(grad_out, g, coords, zero_level_mask, grad_levels); break;
+    case RR: rmd::corr_lookup_backward_kernel<RR><<<grid, rmd::kBwdThreads, 0, st>>>(grad_out, g, coords, zero_level_mask, grad_levels); break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE
         default:

@@ -178,7 +178,7 @@ def otf_lookup(st, coords, radius, mask_costs=()):
 #
 # The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an
 # input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
-# accumulates into ONE dense fp32 gradient G (B, N, T) shared through _CorrState (include/rmd.h,
+# accumulates into ONE dense fp32 gradient G (B, T, N), query-minor, shared through _CorrState (include/rmd.h,
 # rmd_corr_lookup_backward); the pyramid backward then turns G into d fmap1 / d fmap2 with two plain
 # library GEMMs (hipBLASLt, strided, no copies) and the native pool / unpool kernels.
 
@@ -224,9 +224,9 @@ class _CorrPyramidFn(torch.autograd.Function):
             stream = _stream(f1)
             _lib.check(lib.rmd_corr_pool_targets(_ptr(f2), b, c, h, w, levels, scale, _ptr(pooled), stream),
                        "rmd_corr_pool_targets")
-            G = st.grad.view(b, n, t)
-            g1 = torch.bmm(pooled.transpose(1, 2), G.transpose(1, 2))                  # (B, C, N)
-            dpool = torch.bmm(G.transpose(1, 2), f1.view(b, c, n).transpose(1, 2))     # (B, T, C)
+            G = st.grad.view(b, t, n)
+            g1 = torch.bmm(pooled.transpose(1, 2), G)                                   # (B, C, N)
+            dpool = torch.bmm(G, f1.view(b, c, n).transpose(1, 2))                      # (B, T, C)
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")
         st.grad = None
