@@ -140,8 +140,8 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * pyramid's orientation), T = rmd_corr_grad_targets() = sum_l H_l*W_l; level l occupies rows
  * [t_off(l), t_off(l) + H_l*W_l) with t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at row
  * t_off(l) + y*W_l + x, query p in column p.  With P = rmd_corr_pool_targets(fmap2, scale =
- * 1/sqrt(C)) as (B, T, C):
- *   grad_fmap1 (B, C, N) = P^T G    and    dP (B, T, C) = G fmap1^T      (plain GEMMs)
+ * 1/sqrt(C)) as (B, C, T):
+ *   grad_fmap1 (B, C, N) = P G    and    dP (B, C, T) = fmap1 G^T      (plain GEMMs)
  *   grad_fmap2 = rmd_corr_unpool_targets(dP, scale = 1/sqrt(C)).
  */
 
@@ -155,7 +155,7 @@ long long rmd_corr_grad_targets(int height, int width, int levels);
 int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* desc, const float* coords,
                              int radius, unsigned zero_level_mask, float* grad_levels, void* stream);
 
-/* pooled (B, T, C) = avg_pool_{2^l}(fmap2) * scale for every level (raft.py:35-47 applied to the
+/* pooled (B, C, T) = avg_pool_{2^l}(fmap2) * scale for every level (raft.py:35-47 applied to the
  * feature map, which commutes with the product). */
 int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,
                           float scale, float* pooled, void* stream);
@@ -163,6 +163,11 @@ int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int heigh
 /* grad_fmap2 (B, C, H, W) = scale * sum_l avg_pool_{2^l}^T(grad_pooled level l)  (avg_pool2d_backward). */
 int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
                             float scale, float* grad_fmap2, void* stream);
+
+/* hi = bf16(x), lo = bf16(x - hi) elementwise (n floats, 16-B aligned buffers): operands of the
+ * fp32-accurate split-bf16 products hi.hi + hi.lo + lo.hi (the pyramid backward's GEMMs in the fp32
+ * mode run as three bf16 GEMMs with fp32 accumulation). */
+int rmd_split_bf16(const float* x, long long n, void* hi, void* lo, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);

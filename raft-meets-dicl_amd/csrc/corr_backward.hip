@@ -122,16 +122,15 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
     }
 }
 
-// P (B, T, C) = avg-pooled fmap2 / sqrt(C), all levels; one thread per (b, t, c), c fastest
+// P (B, C, T) = avg-pooled fmap2 * scale, all levels; one thread per (b, c, t), t fastest: a wave
+// reads neighbouring target pixels of one channel plane (coalesced) and writes 256 B contiguous
 __global__ void __launch_bounds__(kThreads)
 pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, float scale, float* __restrict__ P) {
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const long long total = (long long)g.batch * g.T * C;
+    const long long total = (long long)g.batch * C * g.T;
     if (idx >= total) return;
-    const int c = (int)(idx % C);
-    const long long bt = idx / C;
-    const long long t = bt % g.T;
-    const int b = (int)(bt / g.T);
+    const long long t = idx % g.T;
+    const long long bc = idx / g.T;              // b * C + c: the channel plane
     int l = 0;
 #pragma unroll
     for (int k = 1; k < RMD_MAX_LEVELS; ++k)
@@ -139,14 +138,14 @@ pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, float scale,
     const int tl = (int)(t - g.toff[l]);
     const int y = tl / g.lw[l], x = tl - y * g.lw[l];
     const int s = 1 << l;
-    const float* src = f + ((size_t)b * C + c) * g.height * g.width + (size_t)(y * s) * g.width + x * s;
+    const float* src = f + (size_t)bc * g.height * g.width + (size_t)(y * s) * g.width + x * s;
     float acc = 0.f;
     for (int dy = 0; dy < s; ++dy)
         for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.width + dx];
     P[idx] = acc * (scale / (float)(s * s));
 }
 
-// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l; one thread per output element
+// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T); one thread per output element
 __global__ void __launch_bounds__(kThreads)
 unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float scale, float* __restrict__ df) {
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
@@ -155,18 +154,42 @@ unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float sca
     if (idx >= total) return;
     const int px = (int)(idx % HW);
     const long long bc = idx / HW;
-    const int c = (int)(bc % C), b = (int)(bc / C);
     const int y = px / g.width, x = px - y * g.width;
-    const float* base = dP + (size_t)b * g.T * C + c;
+    const float* base = dP + (size_t)bc * g.T;
     float acc = 0.f;
 #pragma unroll
     for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
         if (l >= g.levels) break;
         const int yl = y >> l, xl = x >> l;
         if (yl < g.lh[l] && xl < g.lw[l])
-            acc += base[(size_t)(g.toff[l] + (long long)yl * g.lw[l] + xl) * C] * (1.0f / (float)(1 << (2 * l)));
+            acc += base[g.toff[l] + (long long)yl * g.lw[l] + xl] * (1.0f / (float)(1 << (2 * l)));
     }
     df[idx] = acc * scale;
+}
+
+// x = hi + lo, hi = bf16(x), lo = bf16(x - hi): the split operands of the fp32-accurate bf16 GEMMs
+// (hi.hi + hi.lo + lo.hi) of the pyramid backward; 4 elements per thread
+__global__ void __launch_bounds__(kThreads)
+split_bf16_kernel(const float* __restrict__ x, long long n, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
+    const long long i = ((long long)blockIdx.x * kThreads + threadIdx.x) * 4;
+    if (i + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        __bf16 h[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h[k] = (__bf16)e[k];
+            l[k] = (__bf16)(e[k] - (float)h[k]);
+        }
+        *reinterpret_cast<uint2*>(hi + i) = *reinterpret_cast<const uint2*>(h);
+        *reinterpret_cast<uint2*>(lo + i) = *reinterpret_cast<const uint2*>(l);
+    } else {
+        for (long long k = i; k < n; ++k) {
+            const __bf16 h = (__bf16)x[k];
+            hi[k] = h;
+            lo[k] = (__bf16)(x[k] - (float)h);
+        }
+    }
 }
 
 int check_grad_args(int batch, int channels, int h, int w, int levels) {
@@ -214,7 +237,7 @@ extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels
     int rc = rmd::check_grad_args(batch, channels, height, width, levels);
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
-    const long long total = (long long)batch * g.T * channels;
+    const long long total = (long long)batch * channels * g.T;
     rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
                                rmd::as_stream(stream)>>>(fmap2, g, channels, scale, pooled);
     return rmd::check_launch("rmd_corr_pool_targets");
@@ -230,4 +253,15 @@ extern "C" int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int 
     rmd::unpool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
                                  rmd::as_stream(stream)>>>(grad_pooled, g, channels, scale, grad_fmap2);
     return rmd::check_launch("rmd_corr_unpool_targets");
+}
+
+extern "C" int rmd_split_bf16(const float* x, long long n, void* hi, void* lo, void* stream) {
+    RMD_REQUIRE(x && hi && lo, RMD_ERR_ARG, "rmd_split_bf16: null pointer");
+    RMD_REQUIRE(n >= 0 && (((uintptr_t)x | (uintptr_t)hi | (uintptr_t)lo) & 15) == 0, RMD_ERR_ARG,
+                "rmd_split_bf16: n < 0 or pointers not 16-B aligned");
+    if (n == 0) return RMD_OK;
+    const long long threads = (n + 3) / 4;
+    rmd::split_bf16_kernel<<<(unsigned)((threads + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
+                             rmd::as_stream(stream)>>>(x, n, reinterpret_cast<__bf16*>(hi), reinterpret_cast<__bf16*>(lo));
+    return rmd::check_launch("rmd_split_bf16");
 }

@@ -179,14 +179,16 @@ def otf_lookup(st, coords, radius, mask_costs=()):
 # The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an
 # input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
 # accumulates into ONE dense fp32 gradient G (B, T, N), query-minor, shared through _CorrState (include/rmd.h,
-# rmd_corr_lookup_backward); the pyramid backward then turns G into d fmap1 / d fmap2 with two plain
-# library GEMMs (hipBLASLt, strided, no copies) and the native pool / unpool kernels.
+# rmd_corr_lookup_backward); the pyramid backward then turns G into d fmap1 / d fmap2 with two
+# library GEMMs (hipBLASLt; fp32 modes: three split-bf16 products each with fp32 accumulation,
+# fp32-exact: plain fp32) and the native pool / unpool kernels.
 
 class _CorrState:
-    def __init__(self, pyr, f1, f2):
+    def __init__(self, pyr, f1, f2, precision):
         self.pyr = pyr
         self.f1 = f1
         self.f2 = f2
+        self.precision = precision
         self.grad = None          # dense G, allocated by the first lookup backward
 
 
@@ -218,19 +220,49 @@ class _CorrPyramidFn(torch.autograd.Function):
         lib = _lib.lib()
         t = lib.rmd_corr_grad_targets(h, w, levels)
         scale = st.pyr.scale
-        pooled = torch.empty((b, t, c), dtype=torch.float32, device=f1.device)
+        pooled = torch.empty((b, c, t), dtype=torch.float32, device=f1.device)
         g2 = torch.empty_like(f2)
         with torch.cuda.device(f1.device):
             stream = _stream(f1)
             _lib.check(lib.rmd_corr_pool_targets(_ptr(f2), b, c, h, w, levels, scale, _ptr(pooled), stream),
                        "rmd_corr_pool_targets")
             G = st.grad.view(b, t, n)
-            g1 = torch.bmm(pooled.transpose(1, 2), G)                                   # (B, C, N)
-            dpool = torch.bmm(G, f1.view(b, c, n).transpose(1, 2))                      # (B, T, C)
+            f1m = f1.view(b, c, n)
+            if PRECISIONS[st.precision][0] == RMD_F32:
+                g1 = torch.bmm(pooled, G)                                   # (B, C, N)   exact fp32
+                dpool = torch.bmm(f1m, G.transpose(1, 2))                   # (B, C, T)
+            else:
+                Gs = _split(G)                                              # G split once, used twice
+                g1 = _bmm_split(_split(pooled), Gs, st.precision)
+                dpool = _bmm_split(_split(f1m), Gs, st.precision, transpose_b=True)
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")
         st.grad = None
         return g1.view(b, c, h, w), g2, None
+
+
+def _split(x):
+    """x (fp32) -> (hi, lo) bf16 with x ~= hi + lo (rmd_split_bf16)."""
+    x = x.contiguous()
+    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_like(hi)
+    _lib.check(_lib.lib().rmd_split_bf16(_ptr(x), x.numel(), _ptr(hi), _ptr(lo), _stream(x)), "rmd_split_bf16")
+    return hi, lo
+
+
+def _bmm_split(a, b, precision, transpose_b=False):
+    """a (B, M, K) @ b (B, K, N) [or b^T for b (B, N, K)], operands given split (_split), with fp32
+    output from bf16 library GEMMs (hipBLASLt, fp32 accumulation): hi.hi + hi.lo + lo.hi for the
+    fp32 modes, hi.hi for bf16."""
+    ah, al = a
+    bh, bl = b
+    if transpose_b:
+        bh, bl = bh.transpose(1, 2), bl.transpose(1, 2)
+    out = torch.bmm(ah, bh, out_dtype=torch.float32)
+    if PRECISIONS[precision][0] != RMD_BF16:
+        out += torch.bmm(ah, bl, out_dtype=torch.float32)
+        out += torch.bmm(al, bh, out_dtype=torch.float32)
+    return out
 
 
 class _CorrLookupFn(torch.autograd.Function):
@@ -268,8 +300,9 @@ def ctx_desc(st):
 def corr_block_autograd(fmap1, fmap2, levels, precision, scale=None):
     """Pyramid + autograd token for a CorrBlock whose feature maps require gradients."""
     _require_gpu(fmap1, fmap2)
+    precision = precision or _default_precision
     pyr = corr_pyramid(fmap1, fmap2, levels, precision, scale=scale)
-    st = _CorrState(pyr, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous())
+    st = _CorrState(pyr, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous(), precision)
     token = _CorrPyramidFn.apply(fmap1, fmap2, st)
     return pyr, st, token
 
