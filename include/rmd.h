@@ -164,11 +164,6 @@ int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int heigh
 int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
                             float scale, float* grad_fmap2, void* stream);
 
-/* hi = bf16(x), lo = bf16(x - hi) elementwise (n floats, 16-B aligned buffers): operands of the
- * fp32-accurate split-bf16 products hi.hi + hi.lo + lo.hi (the pyramid backward's GEMMs in the fp32
- * mode run as three bf16 GEMMs with fp32 accumulation). */
-int rmd_split_bf16(const float* x, long long n, void* hi, void* lo, void* stream);
-
 /* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);
  * stack (B, d, d, 2C [+2], h, w) float32 contiguous with d = 2r+1, dim 1 the x-offset a-r and

@@ -167,31 +167,6 @@ unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float sca
     df[idx] = acc * scale;
 }
 
-// x = hi + lo, hi = bf16(x), lo = bf16(x - hi): the split operands of the fp32-accurate bf16 GEMMs
-// (hi.hi + hi.lo + lo.hi) of the pyramid backward; 4 elements per thread
-__global__ void __launch_bounds__(kThreads)
-split_bf16_kernel(const float* __restrict__ x, long long n, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
-    const long long i = ((long long)blockIdx.x * kThreads + threadIdx.x) * 4;
-    if (i + 4 <= n) {
-        const float4 v = *reinterpret_cast<const float4*>(x + i);
-        const float e[4] = {v.x, v.y, v.z, v.w};
-        __bf16 h[4], l[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            h[k] = (__bf16)e[k];
-            l[k] = (__bf16)(e[k] - (float)h[k]);
-        }
-        *reinterpret_cast<uint2*>(hi + i) = *reinterpret_cast<const uint2*>(h);
-        *reinterpret_cast<uint2*>(lo + i) = *reinterpret_cast<const uint2*>(l);
-    } else {
-        for (long long k = i; k < n; ++k) {
-            const __bf16 h = (__bf16)x[k];
-            hi[k] = h;
-            lo[k] = (__bf16)(x[k] - (float)h);
-        }
-    }
-}
-
 int check_grad_args(int batch, int channels, int h, int w, int levels) {
     RMD_REQUIRE(batch >= 1 && channels >= 1 && h >= 1 && w >= 1, RMD_ERR_SHAPE, "rmd corr backward: bad sizes");
     RMD_REQUIRE(levels >= 1 && levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd corr backward: bad levels");
@@ -255,13 +230,3 @@ extern "C" int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int 
     return rmd::check_launch("rmd_corr_unpool_targets");
 }
 
-extern "C" int rmd_split_bf16(const float* x, long long n, void* hi, void* lo, void* stream) {
-    RMD_REQUIRE(x && hi && lo, RMD_ERR_ARG, "rmd_split_bf16: null pointer");
-    RMD_REQUIRE(n >= 0 && (((uintptr_t)x | (uintptr_t)hi | (uintptr_t)lo) & 15) == 0, RMD_ERR_ARG,
-                "rmd_split_bf16: n < 0 or pointers not 16-B aligned");
-    if (n == 0) return RMD_OK;
-    const long long threads = (n + 3) / 4;
-    rmd::split_bf16_kernel<<<(unsigned)((threads + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
-                             rmd::as_stream(stream)>>>(x, n, reinterpret_cast<__bf16*>(hi), reinterpret_cast<__bf16*>(lo));
-    return rmd::check_launch("rmd_split_bf16");
-}

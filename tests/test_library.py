@@ -1,0 +1,74 @@
+"""torch.library registration of the rmd operators (SURVEY.md §8(b) op schemas).
+
+CPU: every operator is registered with a schema, its fake (meta) kernel propagates shapes and dtypes
+without a GPU (FakeTensor tracing for torch.compile / export), and real CPU tensors raise (no CPU
+fallback).  GPU (marked): torch.library.opcheck — schema, fake-vs-real outputs, autograd
+registration — on small shapes of every operator family.
+"""
+
+import pytest
+import torch
+
+EXPECTED = ["corr_lookup", "corr_otf_lookup", "corr_otf_prepare", "corr_pyramid", "dap", "dap_transpose",
+            "dicl_stack", "dicl_stack_backward", "dicl_stack_int", "dicl_stack_int_backward", "dicl_stack_int_warped",
+            "dicl_stack_int_warped_backward", "softargmax", "softargmax_backward", "up8", "up8_backward",
+            "warp_backwards", "warp_backwards_backward"]
+
+
+def test_every_operator_registered():
+    from rmd import library
+    assert library.operators() == EXPECTED
+    for name in EXPECTED:
+        assert hasattr(torch.ops.rmd, name)
+
+
+def test_fake_kernels_propagate_shapes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from rmd import _lib
+    with FakeTensorMode():
+        f1 = torch.empty(2, 256, 55, 128, device="cuda")
+        pyr = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16, _lib.RMD_F16, 0.0625)
+        assert pyr.dtype == torch.float16 and pyr.numel() == _lib.describe(2, 55, 128, 4, _lib.RMD_F16).total_elements
+        co = torch.empty(2, 2, 55, 128, device="cuda")
+        assert torch.ops.rmd.corr_lookup(pyr, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        f = torch.empty(2, 32, 12, 16, device="cuda")
+        c2 = torch.empty(2, 2, 12, 16, device="cuda")
+        assert torch.ops.rmd.dicl_stack(f, f, c2, 4, 0, 12, 16, False).shape == (2, 9, 9, 64, 12, 16)
+        assert torch.ops.rmd.dicl_stack(f, f, c2, 4, 0, 12, 16, True).shape == (2, 9, 9, 66, 12, 16)
+        assert torch.ops.rmd.dicl_stack_int(f, f, 3, 3).shape == (2, 7, 7, 64, 12, 16)
+        assert torch.ops.rmd.dap(torch.empty(2, 81, 12, 16, device="cuda"), torch.empty(81, 81, 1, 1, device="cuda")).shape == (2, 81, 12, 16)
+        assert torch.ops.rmd.up8(torch.empty(2, 576, 12, 16, device="cuda"), c2, 4.0).shape == (2, 2, 96, 128)
+        assert torch.ops.rmd.softargmax(torch.empty(2, 324, 12, 16, device="cuda"), 4, 4, 1.0).shape == (4, 2, 2, 12, 16)
+        out, mask = torch.ops.rmd.warp_backwards(f, c2, 1e-5)
+        assert out.shape == f.shape and mask.shape == (2, 1, 12, 16) and mask.dtype == torch.bool
+
+
+def test_cpu_tensors_raise():
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        torch.ops.rmd.dap(torch.zeros(1, 81, 4), torch.zeros(81, 81))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        torch.ops.rmd.dicl_stack_int(torch.zeros(1, 8, 4, 4), torch.zeros(1, 8, 4, 4), 1, 1)
+
+
+@pytest.mark.gpu
+def test_opcheck_operator_families():
+    from rmd import _lib
+    dev = "cuda"
+    g = torch.Generator().manual_seed(0)
+    r = lambda *s: torch.randn(*s, generator=g).to(dev)  # noqa: E731
+    ys, xs = torch.meshgrid(torch.arange(10.0), torch.arange(12.0), indexing="ij")
+    co = (torch.stack([xs, ys])[None].expand(2, -1, -1, -1) + torch.randn(2, 2, 10, 12, generator=g) * 2).to(dev)
+    f1, f2 = r(2, 16, 10, 12), r(2, 16, 10, 12)
+    cases = [
+        (torch.ops.rmd.corr_pyramid, (f1, f2, 3, _lib.RMD_BF16X3, _lib.RMD_F32, 0.25)),
+        (torch.ops.rmd.dicl_stack, (f1.requires_grad_(), f2.requires_grad_(), co, 2, 0, 10, 12, False)),
+        (torch.ops.rmd.dicl_stack_int, (f1, f2, 2, 2)),
+        (torch.ops.rmd.dap, (r(2, 25, 10, 12).requires_grad_(), r(25, 25, 1, 1).requires_grad_())),
+        (torch.ops.rmd.up8, (r(2, 576, 10, 12).requires_grad_(), r(2, 2, 10, 12).requires_grad_(), 4.0)),
+        (torch.ops.rmd.softargmax, (r(2, 81, 10, 12).requires_grad_(), 1, 4, 1.0)),
+    ]
+    for op, args in cases:
+        torch.library.opcheck(op, args, test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+    pyr = torch.ops.rmd.corr_pyramid(f1.detach(), f2.detach(), 3, _lib.RMD_BF16X3, _lib.RMD_F32, 0.25)
+    torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0),
+                          test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))

@@ -7,7 +7,9 @@ mkdir -p gpurun_out
 if [ -z "$SKIPTESTS" ]; then
   timeout -k 10 ${TESTTIME:-900} python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} > gpurun_out/${TAG}_tests.log 2>&1 || exit 3
 fi
-timeout -k 10 400 python3 -u bench.py ${BENCHARGS} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 4
+if [ -z "$SKIPBENCH" ]; then
+  timeout -k 10 400 python3 -u bench.py ${BENCHARGS} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit 4
+fi
 if [ -n "$PROF" ]; then
   R=$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}
   mkdir -p $R
