@@ -97,7 +97,12 @@ class _Dev:
 
 
 def _f32(t):
-    return t.detach().float().contiguous()
+    """fp32, contiguous, detached (no aten.to call for fp32 inputs: an operator below autograd must
+    not hand back its own input)."""
+    t = t.detach()
+    if t.dtype != torch.float32:
+        t = t.to(torch.float32)
+    return t.contiguous()
 
 
 _DESC = {}
