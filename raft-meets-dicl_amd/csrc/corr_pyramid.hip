@@ -1054,6 +1054,43 @@ __device__ __forceinline__ void mma_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16]
     mma_steps_pad<0>(acc, bq, a, smem, b0, b1);
 }
 
+// ---- B-ring variant (RING = true): B fragments stream through an 8-slot register ring ----------
+// k-step s of every tile lives in slot s % 8 and is loaded 7 k-steps (56 MFMAs) ahead — the previous
+// tile's k-steps 9-15 load this tile's 0-6 — instead of all 16 (64 VGPRs) being held for the whole
+// tile; the 32 VGPRs freed double-buffer the A fragments: k-step s+1's 8 fragments are read at the
+// top of k-step s.  One scheduling region per k-step keeps both sets of loads where they are issued.
+constexpr int kRing = 8;
+
+template <int S>
+__device__ __forceinline__ void read_a8(bf16x8 (&a)[8], const unsigned char* smem, unsigned b0, unsigned b1) {
+#pragma unroll
+    for (int ti = 0; ti < 8; ++ti)
+        a[ti] = *reinterpret_cast<const bf16x8*>(smem + ((ti & 1) ? b1 : b0) + (unsigned)((ti >> 1) * 32 * kPadRow + 32 * S));
+}
+
+template <int S>
+__device__ __forceinline__ void ksteps_ring(f32x16 (&acc)[8], bf16x8 (&acur)[8], bf16x8 (&anext)[8],
+                                            bf16x8 (&ring)[kRing], const unsigned char* smem, unsigned b0,
+                                            unsigned b1, const __bf16* cur, const __bf16* nxt) {
+    if constexpr (S < 16) {
+        if constexpr (S + 1 < 16) read_a8<S + 1>(anext, smem, b0, b1);
+        {
+            constexpr int T = S + kRing - 1;
+            ring[T % kRing] = *reinterpret_cast<const bf16x8*>((T < 16 ? cur : nxt) + 512 * (T & 15));
+        }
+        const f32x16 zero = {};
+#pragma unroll
+        for (int ti = 0; ti < 8; ++ti)
+            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[ti], ring[S % kRing], S == 0 ? zero : acc[ti], 0, 0, 0);
+        // order inside the region: the 8 LDS reads of k-step S+1 and the ring load first, then the MFMAs
+        if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        ksteps_ring<S + 1>(acc, anext, acur, ring, smem, b0, b1, cur, nxt);
+    }
+}
+
 template <int S, int AUX>
 __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx& c, const pipe::LaneOff& lo,
                                          pipe::EpiState& st) {
@@ -1065,7 +1102,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx
 
 }  // namespace w8
 
-template <int AUX, bool ROLL, bool PAD = true>
+template <int AUX, bool ROLL, bool PAD = true, bool RING = false, bool PP = false, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
                 __half* __restrict__ pyr, int drop_stores, int stagger) {
@@ -1139,7 +1176,74 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
     const __bf16* gB = opB + ((size_t)b * nqt * 1024 + lane) * 8;
     const int stride = WAVES * qsplit;
     int qt = split * WAVES + w;
+    if constexpr (RING && PP) {
+        // Ping-pong: the two waves of each SIMD (w and w + 4) alternate between an MFMA phase and an
+        // epilogue phase, separated by workgroup barriers, so one wave's pooling VALU and stores run
+        // while its partner owns the matrix pipe (free-running partners drift into lock step: PMC of
+        // the free-running kernel shows VALU co-issued with MFMA in only a third of its VALU cycles).
+        // Waves 4-7 start one phase late; every wave runs 2 * nmax + 1 barriers.
+        const int f0 = split * WAVES;
+        const int nmax = f0 < nqt ? (nqt - f0 + stride - 1) / stride : 0;
+        const int nw = qt < nqt ? (nqt - qt + stride - 1) / stride : 0;
+        const bool late = w >= 4;
+        unsigned b0 = pb0, b1 = pb1;
+        asm volatile("" : "+v"(b0), "+v"(b1));
+        bf16x8 ring[w8::kRing];
+        if (nw > 0) {
+#pragma unroll
+            for (int s = 0; s < w8::kRing - 1; ++s) ring[s] = *reinterpret_cast<const bf16x8*>(gB + (size_t)qt * 8192 + 512 * s);
+        }
+        if (late) __builtin_amdgcn_s_barrier();
+        for (int k = 0; k < nmax; ++k) {
+            f32x16 acc[8];
+            const int qn = qt + stride;
+            if (k < nw) {
+                if constexpr (ABL == 2) {       // diagnostic: no k-loop (epilogue-only timing)
+#pragma unroll
+                    for (int ti = 0; ti < 8; ++ti)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
+                } else {
+                    bf16x8 a0[8], a1[8];
+                    w8::read_a8<0>(a0, smem, b0, b1);
+                    w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
+                                       gB + (size_t)min(qn, nqt - 1) * 8192);
+                }
+            }
+            __builtin_amdgcn_s_barrier();
+            if (k < nw) {
+                const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+                pipe::EpiState st;
+                w8::epilogue<0, AUX>(acc, c, lo, st);
+            }
+            __builtin_amdgcn_s_barrier();
+            qt = qn;
+        }
+        if (!late) __builtin_amdgcn_s_barrier();
+        return;
+    }
     if (qt >= nqt) return;
+    if constexpr (RING) {
+        unsigned b0 = pb0, b1 = pb1;
+        asm volatile("" : "+v"(b0), "+v"(b1));
+        bf16x8 ring[w8::kRing];
+#pragma unroll
+        for (int s = 0; s < w8::kRing - 1; ++s) ring[s] = *reinterpret_cast<const bf16x8*>(gB + (size_t)qt * 8192 + 512 * s);
+        while (true) {
+            f32x16 acc[8];
+            const int qn = qt + stride;
+            bf16x8 a0[8], a1[8];
+            w8::read_a8<0>(a0, smem, b0, b1);
+            w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
+                               gB + (size_t)min(qn, nqt - 1) * 8192);
+            const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+            pipe::EpiState st;
+            w8::epilogue<0, AUX>(acc, c, lo, st);
+            if (qn >= nqt) break;
+            qt = qn;
+        }
+        return;
+    }
     bf16x8 bq[16];
     {
         const __bf16* p0 = gB + (size_t)qt * 8192;
@@ -1256,7 +1360,8 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                 // pyramid is written once and read back a full GEMM later)
                 int qs = 1;
                 while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
-                auto kern = corr_pyramid_w8<2, false, true>;
+                // product: padded LDS A block, B-fragment register ring, ping-pong MFMA / epilogue phases
+                auto kern = corr_pyramid_w8<2, false, true, true, true>;
                 int lds_w8 = 256 * (int)w8::kPadRow;
                 int drop = 0, stagger = 0;
 #ifdef RMD_DIAG
@@ -1266,10 +1371,15 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                     kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true, false> : corr_pyramid_w8<2, false, false>)
                                     : (roll ? corr_pyramid_w8<0, true, false> : corr_pyramid_w8<0, false, false>);
                     lds_w8 = lds;
-                } else if (aux != 2) {
-                    kern = corr_pyramid_w8<0, false, true>;
+                } else if (env_knob("RMD_W8_RING", 2) == 2) {
+                    if (env_knob("RMD_ABLATE", 0) >= 2) kern = corr_pyramid_w8<2, false, true, true, true, 2>;
+                    else if (aux != 2) kern = corr_pyramid_w8<0, false, true, true, true>;
+                } else if (env_knob("RMD_W8_RING", 2) == 1) {
+                    kern = corr_pyramid_w8<2, false, true, true>;
+                } else {
+                    kern = aux == 2 ? corr_pyramid_w8<2, false, true> : corr_pyramid_w8<0, false, true>;
                 }
-                drop = env_knob("RMD_ABLATE", 0) == 1;
+                drop = env_knob("RMD_ABLATE", 0) == 1 || env_knob("RMD_ABLATE", 0) == 3;
                 stagger = env_knob("RMD_W8_STAGGER", 0);
 #endif
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds_w8);

@@ -36,6 +36,9 @@ def main():
         kern, _, knobs = kern.partition("+")        # e.g. "w8+roll+stag4" = RMD_W8_ROLL=1, RMD_W8_STAGGER=4
         os.environ["RMD_W8_ROLL"] = "1" if "roll" in knobs else "0"
         os.environ["RMD_W8_PAD"] = "0" if "nopad" in knobs else "1"      # "w8+nopad" = XOR-swizzled LDS
+        # "w8+ring" = B ring + double-buffered A; "w8+pp" = the same with ping-pong phases (barriers)
+        # (default w8 = the product kernel: padded LDS + ring + ping-pong; "w8+plain" = neither)
+        os.environ["RMD_W8_RING"] = "1" if "ring" in knobs else ("0" if "plain" in knobs or "nopad" in knobs else "2")
         stag = int(knobs.split("stag")[1].split("+")[0]) if "stag" in knobs else 0
         os.environ["RMD_W8_STAGGER"] = str(stag + (1000 if "prio" in knobs else 0))     # "w8+prio" = s_setprio 1 on waves 4-7
         os.environ["RMD_GEMM_KERNEL"] = kern
