@@ -717,6 +717,33 @@ struct EpiState {
 
 #define V(acc, row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)])
 
+// Store context of block (rb, cb) for query tile qt in the query-tile-major layout (diagnostic
+// experiment): level l element (b, qt, y, xc, j, e) at off_l + ((((b NQT + qt) H_l + y) TX_l + xc) 32 + j) cw + e
+__device__ __forceinline__ Ctx ctx_qtm(const PyrGeom& g, int b, int qt, int rb, int cb, __half* pyr) {
+    Ctx c;
+    const int nqt = (g.height * g.width + 31) >> 5;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
+        const int y0 = rb * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        const int cw = g.tw[l];
+        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * 32u * cw * 2u : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] + ((((size_t)b * nqt + qt) * g.ty[l] + y0) * g.tx[l] + xc0) * 32 * cw) : 0;
+        __half* bp = pyr + base;
+        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+                                                        (int)__builtin_amdgcn_readfirstlane((unsigned)rows * rs), 0x00020000);
+        c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
+        c.l[l].cs = __builtin_amdgcn_readfirstlane(32u * cw * 2u);
+        c.l[l].cw2 = (unsigned)cw * 2u;
+        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+    }
+    return c;
+}
+
 // Epilogue piece s (0..15) of one tile, from accumulator set `acc` (see the block comment).
 template <int S, int AUX = 0>
 __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, const LaneOff& lo, EpiState& st) {
@@ -1198,7 +1225,7 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
             f32x16 acc[8];
             const int qn = qt + stride;
             if (k < nw) {
-                if constexpr (ABL == 2) {       // diagnostic: no k-loop (epilogue-only timing)
+                if constexpr (ABL == 2 || ABL == 4) {       // diagnostic: no k-loop (epilogue-only timing)
 #pragma unroll
                     for (int ti = 0; ti < 8; ++ti)
 #pragma unroll
@@ -1212,9 +1239,16 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
             }
             __builtin_amdgcn_s_barrier();
             if (k < nw) {
-                const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
-                pipe::EpiState st;
-                w8::epilogue<0, AUX>(acc, c, lo, st);
+                if constexpr (ABL >= 4) {       // diagnostic: query-tile-major store layout (timing only)
+                    const pipe::Ctx ct = pipe::ctx_qtm(g, b, qt, rb, cb, pyr);
+                    const pipe::LaneOff lo = pipe::lane_offsets(ct, j, h, true);
+                    pipe::EpiState st;
+                    w8::epilogue<0, AUX>(acc, ct, lo, st);
+                } else {
+                    const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+                    pipe::EpiState st;
+                    w8::epilogue<0, AUX>(acc, c, lo, st);
+                }
             }
             __builtin_amdgcn_s_barrier();
             qt = qn;
@@ -1372,7 +1406,9 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                                     : (roll ? corr_pyramid_w8<0, true, false> : corr_pyramid_w8<0, false, false>);
                     lds_w8 = lds;
                 } else if (env_knob("RMD_W8_RING", 2) == 2) {
-                    if (env_knob("RMD_ABLATE", 0) >= 2) kern = corr_pyramid_w8<2, false, true, true, true, 2>;
+                    if (env_knob("RMD_ABLATE", 0) == 4) kern = corr_pyramid_w8<2, false, true, true, true, 4>;
+                    else if (env_knob("RMD_ABLATE", 0) == 5) kern = corr_pyramid_w8<2, false, true, true, true, 5>;
+                    else if (env_knob("RMD_ABLATE", 0) >= 2) kern = corr_pyramid_w8<2, false, true, true, true, 2>;
                     else if (aux != 2) kern = corr_pyramid_w8<0, false, true, true, true>;
                 } else if (env_knob("RMD_W8_RING", 2) == 1) {
                     kern = corr_pyramid_w8<2, false, true, true>;

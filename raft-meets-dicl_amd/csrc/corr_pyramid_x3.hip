@@ -219,7 +219,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
     }
 }
 
-constexpr int kRing = 4;     // B ring slots (16 % kRing == 0: k-step s of every tile maps to slot s % kRing)
+constexpr int kRing = 8;     // B ring slots (16 % kRing == 0: k-step s of every tile maps to slot s % kRing)
 
 // A fragments (hi in [2ti], lo in [2ti+1]) of k-step S for the 4 target tiles
 template <int S>
@@ -255,11 +255,17 @@ __device__ __forceinline__ void ksteps(f32x16 (&acc)[4], bf16x8 (&acur)[8], bf16
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bl, c, 0, 0, 0);
             acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bh, c, 0, 0, 0);
         }
+        // order inside the region: k-step S+1's 8 LDS reads and the 2 ring loads first, then 12 MFMAs
+        if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
         __builtin_amdgcn_sched_barrier(0);      // one scheduling region per k-step
         ksteps<S + 1>(acc, anext, acur, rh, rl, smem, b0, b1, curH, curL, nxtH, nxtL);
     }
 }
 
+// ABL (diagnostic build only): 1 = drop every store (descriptor range 0), 2 = no k-loop (epilogue only)
+template <bool PP, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
                 const __bf16* __restrict__ bLo, PyrGeom g, int qsplit, float* __restrict__ pyr) {
@@ -307,7 +313,8 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
         const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
         const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
         L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
-                                                      (int)__builtin_amdgcn_readfirstlane((unsigned)rows * rs), 0x00020000);
+                                                      (int)__builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs),
+                                                      0x00020000);
         L[l].rs = __builtin_amdgcn_readfirstlane(rs);
         L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
         L[l].rows = __builtin_amdgcn_readfirstlane(rows);
@@ -322,18 +329,53 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
     const size_t bb = ((size_t)b * nqt * 1024 + lane) * 8;
     const int stride = WAVES * qsplit;
     int qt = split_ * WAVES + w;
-    if (qt >= nqt) return;
-    // B fragments stream through a 4-slot register ring: k-step s of a tile lives in slot s % 4 and is
-    // loaded at k-step s - 3 (the previous tile's k-steps 13-15 load this tile's 0-2), ~3 k-steps
-    // (36 MFMAs) ahead; A fragments of k-step s + 1 are read from LDS at the top of k-step s.  Each
+    if constexpr (!PP) {
+        if (qt >= nqt) return;
+    }
+    // B fragments stream through an 8-slot register ring: k-step s of a tile lives in slot s % 8 and is
+    // loaded at k-step s - 7 (the previous tile's k-steps 9-15 load this tile's 0-6), 7 k-steps
+    // (84 MFMAs) ahead; A fragments of k-step s + 1 are read from LDS at the top of k-step s.  Each
     // k-step is one scheduling region, so neither set of loads drifts to just before its MFMAs.
     const __bf16* pb = bHi + bb + (size_t)qt * 8192;
     const __bf16* pbl = bLo + bb + (size_t)qt * 8192;
     bf16x8 rh[kRing], rl[kRing];
+    if (qt < nqt) {
 #pragma unroll
-    for (int s = 0; s < kRing - 1; ++s) {
-        rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
-        rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
+        for (int s = 0; s < kRing - 1; ++s) {
+            rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
+            rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
+        }
+    }
+    if constexpr (PP) {
+        // ping-pong phases (as corr_pyramid_w8): waves w and w + 4 of each SIMD alternate between the
+        // MFMA phase and the epilogue phase, separated by workgroup barriers; 2 * nmax + 1 per wave
+        const int f0 = split_ * WAVES;
+        const int nmax = f0 < nqt ? (nqt - f0 + stride - 1) / stride : 0;
+        const int nw = qt < nqt ? (nqt - qt + stride - 1) / stride : 0;
+        const bool late = w >= 4;
+        if (late) __builtin_amdgcn_s_barrier();
+        for (int k = 0; k < nmax; ++k) {
+            f32x16 acc[4];
+            const int qn = qt + stride;
+            if (k < nw && ABL == 2) {
+#pragma unroll
+                for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
+            } else if (k < nw) {
+                const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+                bf16x8 a0[8], a1[8];
+                read_a<0>(a0, smem, b0, b1);
+                ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192, bLo + bb + (size_t)qt * 8192,
+                          bHi + bb + pn, bLo + bb + pn);
+            }
+            __builtin_amdgcn_s_barrier();
+            if (k < nw) epilogue(acc, L, min(qt * 32 + j, N - 1), h);
+            __builtin_amdgcn_s_barrier();
+            qt = qn;
+        }
+        if (!late) __builtin_amdgcn_s_barrier();
+        return;
     }
     while (true) {
         f32x16 acc[4];
@@ -387,10 +429,18 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
     int qs = 1;
     while (nblk * d.batch * qs < 256 && qs * 16 <= nqt) qs *= 2;
+    qs = env_knob("RMD_X3_QS", qs);
     const int lds = kBlockRows * kBlockCols * kRow;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_x3), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    corr_pyramid_x3<<<nblk * d.batch * qs, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), qs,
-                                                           reinterpret_cast<float*>(pyr));
+    // product: ping-pong phases; the diagnostic build's RMD_X3_PP=0 runs free-running waves (A/B)
+#ifdef RMD_DIAG
+    auto kern = env_knob("RMD_X3_PP", 1) ? corr_pyramid_x3<true> : corr_pyramid_x3<false>;
+    if (env_knob("RMD_ABLATE", 0) == 1) kern = corr_pyramid_x3<true, 1>;
+    if (env_knob("RMD_ABLATE", 0) == 2) kern = corr_pyramid_x3<true, 2>;
+#else
+    auto kern = corr_pyramid_x3<true>;
+#endif
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    kern<<<nblk * d.batch * qs, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), qs, reinterpret_cast<float*>(pyr));
     return check_launch("rmd_corr_pyramid/gemm-x3");
 }
 
