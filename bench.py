@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=6, help="frame pairs per GPU (train/chairs2-1 stage)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 (pair with --backend gloo)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/collective plumbing only (no GPU work): for the CPU gloo tests")
     return ap.parse_args()
@@ -290,7 +292,7 @@ def init_distributed(args):
     if args.dry_run:
         device = torch.device("cpu")
     else:
-        device = torch.device("cuda", local)
+        device = torch.device("cuda", 0 if args.one_device else local)
         torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
