@@ -253,7 +253,7 @@ def train_leg(args, world, rank, device):
     if world > 1:
         torch.distributed.barrier()
     el = job_time(el, world, device)
-    last = float(loss)
+    last = float(loss.detach())
     del model, net, opt
     torch.cuda.empty_cache()
     return {"workload": "RAFT+DICL ctf-l3 training step (BASELINE configs[4], SURVEY cfg5): 368x496 padded "
@@ -261,7 +261,8 @@ def train_leg(args, world, rank, device):
             "frame_pairs_per_s": world * bsz * args.train_steps / el, "steps_per_s": args.train_steps / el,
             "ms_per_step": el / args.train_steps * 1e3, "per_gpu_batch": bsz, "global_batch": world * bsz,
             "n_gpus": world, "steps": args.train_steps, "warmup": args.train_warmup,
-            "parallelism": f"DDP x{world} (RCCL bucketed gradient all-reduce)" if world > 1 else "single GPU",
+            "parallelism": (f"DDP x{world} ({'RCCL' if args.backend == 'nccl' else args.backend} bucketed gradient "
+                            f"all-reduce)" if world > 1 else "single GPU"),
             "gradient_bytes_per_step": 4 * n_params, "parameters": n_params, "last_loss": last,
             "scaling": "weak", "dtype": "fp32", "data": "synthetic smooth pairs with known flow, name-keyed random weights"}
 
