@@ -217,6 +217,118 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     }
 }
 
+// Row-exchange variant (diagnostic build, RMD_LOOKUP_XCH=1): one workgroup = 3 waves over the same 64
+// queries and level.  Wave w owns output rows [w*D/3, (w+1)*D/3) and loads only the patch rows no
+// other wave loads: wave 0 rows 0..ob1, wave w > 0 rows ob0+1..ob1.  The one row a wave w > 0 also
+// needs (its first output row's upper row, loaded by wave w-1) is handed over as the horizontally
+// interpolated row (D floats per lane) through 2*D*64*4 bytes of LDS after one barrier; the wave
+// stores all other rows before it.  A window thus loads its 2r+2 patch rows once (10 for r = 4)
+// instead of 3*(PR+1) = 12 for the independent 3-way split, at the same 3 waves per (64 queries, level).
+template <typename T, int R, int L>
+__device__ __forceinline__ void lookup_level_xch(const T* __restrict__ pyr, const PyrGeom& g, int b, int p, int N,
+                                                 float x, float y, unsigned zmask, float* __restrict__ o,
+                                                 bool active, int w, int lane, float* __restrict__ xch) {
+    constexpr int D = 2 * R + 1;
+    constexpr int K = 2 * R + 2;
+    constexpr int KRM = (D + 2) / 3 + 1;                           // most patch rows one wave loads
+    const int ob0 = (w * D) / 3, ob1 = ((w + 1) * D) / 3;          // output rows [ob0, ob1)
+    const int lh = g.lh[L], lw = g.lw[L];
+    // the early exits depend on the level only: uniform over the workgroup, taken before the barrier
+    if ((zmask >> L) & 1u) {
+        if (active)
+            for (int bb = ob0; bb < ob1; ++bb)
+                for (int a = 0; a < D; ++a) __builtin_nontemporal_store(0.f, o + (size_t)(a * D + bb) * N);
+        return;
+    }
+    if (lh < 2 || lw < 2) {     // the reference normalises by (size-1) = 0 -> NaN (raft.py:73-74)
+        if (active)
+            for (int bb = ob0; bb < ob1; ++bb)
+                for (int a = 0; a < D; ++a)
+                    __builtin_nontemporal_store(__builtin_nanf(""), o + (size_t)(a * D + bb) * N);
+        return;
+    }
+    const float inv = 1.0f / (float)(1 << L);
+    float cx = x * inv, cy = y * inv;
+    cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+    cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+    const float fx0 = floorf(cx), fy0 = floorf(cy);
+    const float fx = cx - fx0, fy = cy - fy0;
+    const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+
+    const T* lvl = pyr + g.off[L];
+    constexpr int CW = level_chunk(L);
+    const long long chunk_stride = (long long)N * CW;
+    const long long bq = (long long)b * lh;
+    const int txs = g.tx[L];
+
+    const int r0 = w == 0 ? 0 : ob0 + 1;                            // patch rows [r0, ob1]
+    float hprev[D], hfirst[D];
+#pragma unroll
+    for (int jj = 0; jj < KRM; ++jj) {
+        const int j = r0 + jj;
+        if (j <= ob1) {                                             // wave-uniform
+            const int yy = ys + j;
+            const bool row_ok = yy >= 0 && yy < lh;
+            const int yc = min(max(yy, 0), lh - 1);
+            const T* row_ptr = lvl + ((bq + yc) * txs) * chunk_stride + (long long)p * CW;
+            float v[K];
+            load_row<T, R, CW, 0>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
+            float hcur[D];
+#pragma unroll
+            for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
+            if (jj > 0 && active) {
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+                    __builtin_nontemporal_store(fmaf(fy, hcur[a] - hprev[a], hprev[a]),
+                                                o + (size_t)(a * D + j - 1) * N);
+            }
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                if (jj == 0) hfirst[a] = hcur[a];
+                hprev[a] = hcur[a];
+            }
+        }
+    }
+    if (w < 2) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) xch[(w * D + a) * 64 + lane] = hprev[a];   // row ob1
+    }
+    __syncthreads();
+    if (w > 0 && active) {
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            const float up = xch[((w - 1) * D + a) * 64 + lane];            // row ob0
+            __builtin_nontemporal_store(fmaf(fy, hfirst[a] - up, up), o + (size_t)(a * D + ob0) * N);
+        }
+    }
+}
+
+// grid: (query blocks of 64, batch, level); block: 3 waves (row parts of one window)
+template <typename T, int R>
+__global__ void __launch_bounds__(192)
+corr_lookup_xch_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
+                       float* __restrict__ out) {
+    constexpr int D = 2 * R + 1;
+    __shared__ float xch[2 * D * 64];
+    const int N = g.height * g.width;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int p = blockIdx.x * 64 + lane;
+    const int b = blockIdx.y;
+    const int L = blockIdx.z;
+    const bool active = p < N;
+    const int pc = active ? p : N - 1;
+    const float x = coords[((size_t)b * 2 + 0) * N + pc];
+    const float y = coords[((size_t)b * 2 + 1) * N + pc];
+    float* o = out + ((size_t)b * g.levels + L) * D * D * N + pc;
+    switch (L) {
+        case 0: lookup_level_xch<T, R, 0>(pyr, g, b, pc, N, x, y, zmask, o, active, w, lane, xch); break;
+        case 1: lookup_level_xch<T, R, 1>(pyr, g, b, pc, N, x, y, zmask, o, active, w, lane, xch); break;
+        case 2: lookup_level_xch<T, R, 2>(pyr, g, b, pc, N, x, y, zmask, o, active, w, lane, xch); break;
+        default: lookup_level_xch<T, R, 3>(pyr, g, b, pc, N, x, y, zmask, o, active, w, lane, xch); break;
+    }
+}
+
 template <typename T>
 int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coords, int radius, unsigned zmask,
                   float* out, hipStream_t st) {
@@ -254,6 +366,23 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
             else corr_lookup_kernel<T, 4, 0, 3><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out);
             return check_launch("rmd_corr_lookup");
         }
+    }
+#endif
+#ifdef RMD_DIAG
+    // RMD_LOOKUP_XCH=1: the row-exchange kernel (each patch row loaded once, 10 instead of 12 rows
+    // per r = 4 window).  cfg2 A/B (profiles/lookup_xch_r02.json): 24.56 vs 24.00 us (bf16), 32.1 vs
+    // 32.2 (fp32) — the split's duplicated rows are L2 hits, and the barrier costs more than they do.
+    if (env_knob("RMD_LOOKUP_XCH", 0) != 0) {
+        const dim3 gx((N + 63) / 64, d.batch, d.levels);
+        switch (radius) {
+#define RMD_CASE(RR) case RR: corr_lookup_xch_kernel<T, RR><<<gx, 192, 0, st>>>(p, g, coords, zmask, out); break;
+            RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
+#undef RMD_CASE
+            default:
+                set_error("rmd_corr_lookup: radius %d not in 1..8", radius);
+                return RMD_ERR_SHAPE;
+        }
+        return check_launch("rmd_corr_lookup");
     }
 #endif
     // Product path: non-temporal output stores, and every radius splits a window's 2r+1 output rows
