@@ -94,6 +94,53 @@ def dicl_stack_int(f1, f2, ru, rv):
     return mvol * valid[:, :, :, None]
 
 
+def dicl_stack_int_at(f1, f2, ru, rv, idx):
+    """dicl_stack_int evaluated only at sampled positions (full-size parity checks).
+
+    idx = (b, i, j, y, x) integer arrays of equal length n -> (n, 2C): the same copy + occlusion
+    mask as dicl_stack_int (src/models/impls/dicl.py:212-238), one displacement vector per sample.
+    """
+    b, i, j, y, x = (np.asarray(a, dtype=np.int64) for a in idx)
+    c, h, w = f1.shape[1:]
+    di, dj = i - ru, j - rv
+    xx, yy = x + di, y + dj
+    inside = (xx >= 0) & (xx < w) & (yy >= 0) & (yy < h)
+    v1 = f1[b, :, y, x]                                                   # (n, C)
+    v2 = f2[b, :, np.clip(yy, 0, h - 1), np.clip(xx, 0, w - 1)] * inside[:, None]
+    out = np.concatenate([v1 * inside[:, None], v2], axis=1)
+    valid = v2.sum(axis=1) != 0
+    return out * valid[:, None]
+
+
+def dicl_stack_at(f1, f2, coords, radius, idx, level=0, norm_hw=None):
+    """dicl_stack evaluated only at sampled positions: idx = (b, a, bb, y, x) -> (n, 2C).
+
+    Same sample position as dicl_stack (src/models/common/corr/dicl.py:26-54; level scaling of
+    src/models/impls/raft_dicl_ml.py:294-315): ((x_c/2^i + a - r) * sx, (y_c/2^i + bb - r) * sy),
+    bilinear with zero padding per tap.
+    """
+    b, a, bb, y, x = (np.asarray(t, dtype=np.int64) for t in idx)
+    _, c, h, w = f1.shape
+    hl, wl = f2.shape[-2:]
+    nh, nw = norm_hw if norm_hw is not None else (h, w)
+    s = 2.0 ** level
+    sx = (wl - 1) / (nw - 1)
+    sy = (hl - 1) / (nh - 1)
+    px = (coords[b, 0, y, x] / s + (a - radius)) * sx
+    py = (coords[b, 1, y, x] / s + (bb - radius)) * sy
+    x0, y0 = np.floor(px), np.floor(py)
+    fx, fy = (px - x0)[:, None], (py - y0)[:, None]
+    x0, y0 = x0.astype(np.int64), y0.astype(np.int64)
+
+    def tap(yy, xx):
+        ok = (xx >= 0) & (xx < wl) & (yy >= 0) & (yy < hl)
+        return f2[b, :, np.clip(yy, 0, hl - 1), np.clip(xx, 0, wl - 1)] * ok[:, None]
+
+    samp = ((1 - fx) * (1 - fy) * tap(y0, x0) + fx * (1 - fy) * tap(y0, x0 + 1) +
+            (1 - fx) * fy * tap(y0 + 1, x0) + fx * fy * tap(y0 + 1, x0 + 1))
+    return np.concatenate([f1[b, :, y, x], samp], axis=1)
+
+
 def dicl_stack_int_backward(f1, f2, ru, rv, grad_mvol):
     """Gradients of dicl_stack_int w.r.t. f1, f2 (mask is detached, dicl.py:236)."""
     b, c, h, w = f1.shape

@@ -147,11 +147,13 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
         return;
     }
     const float inv = 1.0f / (float)(1 << L);
-    float cx = x * inv, cy = y * inv;
-    cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
-    cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+    const float rx = x * inv, ry = y * inv;
+    const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f), cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
     const float fx0 = floorf(cx), fy0 = floorf(cy);
-    const float fx = cx - fx0, fy = cy - fy0;
+    // weights from the unclamped coordinate: NaN / +-inf give a NaN weight and so a NaN window, as
+    // the reference's grid_sample does (tests/golden corr_b2_c16_12x20_nonfinite); finite
+    // coordinates beyond +-1e6 have weight 0 either way and read nothing (window off the map)
+    const float fx = rx - floorf(rx), fy = ry - floorf(ry);
     const int xs = (int)fx0 - R, ys = (int)fy0 - R;
 
     const T* lvl = pyr + g.off[L];
@@ -248,11 +250,13 @@ __device__ __forceinline__ void lookup_level_xch(const T* __restrict__ pyr, cons
         return;
     }
     const float inv = 1.0f / (float)(1 << L);
-    float cx = x * inv, cy = y * inv;
-    cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
-    cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+    const float rx = x * inv, ry = y * inv;
+    const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f), cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
     const float fx0 = floorf(cx), fy0 = floorf(cy);
-    const float fx = cx - fx0, fy = cy - fy0;
+    // weights from the unclamped coordinate: NaN / +-inf give a NaN weight and so a NaN window, as
+    // the reference's grid_sample does (tests/golden corr_b2_c16_12x20_nonfinite); finite
+    // coordinates beyond +-1e6 have weight 0 either way and read nothing (window off the map)
+    const float fx = rx - floorf(rx), fy = ry - floorf(ry);
     const int xs = (int)fx0 - R, ys = (int)fy0 - R;
 
     const T* lvl = pyr + g.off[L];

@@ -253,14 +253,15 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
         if (tid < kQ) {
             // query's window origin at level L (coords clamped as rmd_corr_lookup does)
             const float inv = 1.0f / (float)(1 << L);
-            const float cx = fminf(fmaxf(cx0 * inv, -1.0e6f), 1.0e6f);
-            const float cy = fminf(fmaxf(cy0 * inv, -1.0e6f), 1.0e6f);
+            const float rx = cx0 * inv, ry = cy0 * inv;
+            const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f);
+            const float cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
             const float fx0 = floorf(cx), fy0 = floorf(cy);
             const int xs = (int)fx0 - R, ys = (int)fy0 - R;
             sxs[tid] = xs;
             sys[tid] = ys;
-            sfx[tid] = cx - fx0;
-            sfy[tid] = cy - fy0;
+            sfx[tid] = rx - floorf(rx);                // NaN / inf coordinate -> NaN window (grid_sample)
+            sfy[tid] = ry - floorf(ry);
             atomicMin(&box[0], xs);
             atomicMax(&box[1], xs + K - 1);
             atomicMin(&box[2], ys);
@@ -384,7 +385,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             const int q = idx % kQ, a = idx / kQ;
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y >= g.H || x >= g.W) continue;
-            const float fy = sfy[q];
+            const float fy = sfy[q] + (sfx[q] - sfx[q]);   // a NaN x weight reaches rows outside the band too
             if (ablate & 1) {
                 if (hx[i][0] == 123.f) ob[0] = fy;       // keep the sums live
                 continue;

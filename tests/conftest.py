@@ -36,3 +36,18 @@ def rel_max_err(got, ref):
         return 0.0
     scale = np.abs(ref[fin]).max()
     return float(np.abs(got[fin] - ref[fin]).max() / max(scale, 1e-30))
+
+
+def assert_close_elementwise(got, ref, rtol, atol):
+    """Elementwise |got - ref| <= atol + rtol * |ref| (NaN patterns must match); reports the worst entry."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), "NaN pattern differs"
+    fin = np.isfinite(ref)
+    err = np.abs(got[fin] - ref[fin])
+    lim = atol + rtol * np.abs(ref[fin])
+    if err.size and not (err <= lim).all():
+        k = int(np.argmax(err - lim))
+        raise AssertionError(f"elementwise tolerance exceeded at flat {k}: got {got[fin][k]!r} ref {ref[fin][k]!r} "
+                             f"err {err[k]:.3e} > {lim[k]:.3e} ({int((err > lim).sum())} of {err.size} entries)")

@@ -33,9 +33,10 @@ def _grid_coords(rng, b, h, w, spread):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_otf_matches_reference_golden(precision):
+@pytest.mark.parametrize("name", ["corr_fs_b2_c32_24x40", "corr_fs_b2_c16_16x24_nonfinite"])
+def test_otf_matches_reference_golden(precision, name):
     import rmd
-    g = load_golden("corr_fs_b2_c32_24x40")
+    g = load_golden(name)
     cb = rmd.raft_fs.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), int(g["levels"]), int(g["radius"]),
                                precision=precision, method="otf")
     out = cb(_t(g["coords"]))
