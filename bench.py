@@ -42,7 +42,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=8, help="frame pairs per GPU")
+    ap.add_argument("--batch", type=int, default=8, help="frame pairs per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many frame pairs in total, split evenly over the ranks "
+                         "(overrides --batch; must be a multiple of the rank count)")
     ap.add_argument("--height", type=int, default=436)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--channels", type=int, default=256)
@@ -279,8 +282,14 @@ def job_time(elapsed, world, device):
     return float(t.item())
 
 
-def rank_inputs(args, rank, h8, w8, device):
-    """Each rank's own batch of frame pairs (weak scaling: per-rank work fixed, seeds differ)."""
+def rank_inputs(args, rank, world, h8, w8, device):
+    """Weak scaling: each rank's own batch of frame pairs (per-rank work fixed, seeds differ).
+    Strong scaling (--global-batch G): rank r's contiguous G/world shard of one global batch."""
+    if args.global_batch:
+        b = args.global_batch // world
+        f1, f2, co = synthetic(args.global_batch, args.channels, h8, w8, args.iters, 1234, "cpu")
+        sl = slice(rank * b, (rank + 1) * b)
+        return f1[sl].to(device), f2[sl].to(device), co[:, sl].contiguous().to(device)
     return synthetic(args.batch, args.channels, h8, w8, args.iters, 1234 + rank, device)
 
 
@@ -311,6 +320,10 @@ def main():
     world, rank, device = init_distributed(args)
     H, W = padded(args.height, args.width)
     h8, w8 = H // 8, W // 8
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"bench.py: --global-batch {args.global_batch} is not a multiple of {world} ranks")
+        args.batch = args.global_batch // world
     B = args.batch
     N = h8 * w8
     D = (2 * args.radius + 1) ** 2
@@ -322,7 +335,7 @@ def main():
             return None
     else:
         from rmd import ops
-        f1, f2, coords = rank_inputs(args, rank, h8, w8, device)
+        f1, f2, coords = rank_inputs(args, rank, world, h8, w8, device)
         stream = torch.cuda.current_stream(device)
 
         def step(record):
@@ -370,7 +383,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
         "dtype": compute_dt,
         "data": "synthetic (seeded random 1/8-res feature maps + smooth moving flow; no dataset)",

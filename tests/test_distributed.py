@@ -39,9 +39,15 @@ def _job_time_worker(rank, world, port, q):
     _init(rank, world, port)
     try:
         t = bench.job_time(0.5 + rank, world, torch.device("cpu"))
-        args = argparse.Namespace(batch=2, channels=8, iters=3)
-        f1, _, co = bench.rank_inputs(args, rank, 5, 6, torch.device("cpu"))
-        q.put((rank, t, float(f1.sum()), tuple(co.shape)))
+        args = argparse.Namespace(batch=2, channels=8, iters=3, global_batch=0)
+        f1, _, co = bench.rank_inputs(args, rank, world, 5, 6, torch.device("cpu"))
+        # strong scaling: the ranks' shards are the consecutive slices of one global batch of 4
+        sargs = argparse.Namespace(batch=0, channels=8, iters=3, global_batch=4)
+        s1, _, sco = bench.rank_inputs(sargs, rank, world, 5, 6, torch.device("cpu"))
+        g1, _, gco = bench.synthetic(4, 8, 5, 6, 3, 1234, "cpu")
+        strong_ok = (tuple(s1.shape) == (2, 8, 5, 6) and torch.equal(s1, g1[2 * rank: 2 * rank + 2])
+                     and torch.equal(sco, gco[:, 2 * rank: 2 * rank + 2]))
+        q.put((rank, t, float(f1.sum()), tuple(co.shape), strong_ok))
     finally:
         dist.destroy_process_group()
 
@@ -60,6 +66,7 @@ def test_bench_job_time_is_max_over_ranks_and_shards_differ():
     assert [r[1] for r in res] == [1.5, 1.5]          # both ranks report the slowest rank's time
     assert res[0][2] != res[1][2]                     # each rank has its own frame pairs
     assert res[0][3] == (3, 2, 2, 5, 6)
+    assert res[0][4] and res[1][4]                    # strong-scaling shards tile the global batch
 
 
 class _TinyCorrNet(torch.nn.Module):
@@ -148,6 +155,22 @@ def test_bench_launches_its_own_ranks(world):
     res = json.loads(lines[0])
     assert res["n_gpus"] == world and res["config"]["global_batch"] == 8 * world
     assert res["steps"] == 2 and res["scaling"] == "weak"
+
+
+def test_bench_strong_scaling_split():
+    """--global-batch 8 over 2 ranks: 4 pairs per rank, scaling "strong", value counts 8 per step."""
+    import json
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--backend", "gloo", "--no-cpu-baseline", "--steps", "2", "--warmup", "1",
+                          "--global-batch", "8"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["scaling"] == "strong" and res["config"]["global_batch"] == 8
+    assert res["config"]["batch_per_gpu"] == 4
+    assert abs(res["value"] - 8 * 2 / (res["ms_per_step"] * 2 / 1e3)) < 1e-6 * res["value"]
 
 
 def test_bench_rejects_world_size_mismatch():
