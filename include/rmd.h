@@ -141,7 +141,7 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * [t_off(l), t_off(l) + H_l*W_l) with t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at row
  * t_off(l) + y*W_l + x, query p in column p.  With P = rmd_corr_pool_targets(fmap2, scale =
  * 1/sqrt(C)) as (B, C, T):
- *   grad_fmap1 (B, C, N) = P G    and    dP (B, C, T) = fmap1 G^T      (plain GEMMs)
+ *   grad_fmap1 (B, C, N) = P G    and    dP (B, C, T) = fmap1 G^T      (rmd_corr_grad_gemm)
  *   grad_fmap2 = rmd_corr_unpool_targets(dP, scale = 1/sqrt(C)).
  */
 
@@ -163,6 +163,18 @@ int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int heigh
 /* grad_fmap2 (B, C, H, W) = scale * sum_l avg_pool_{2^l}^T(grad_pooled level l)  (avg_pool2d_backward). */
 int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
                             float scale, float* grad_fmap2, void* stream);
+
+/* The two GEMMs of the backward (autograd of the matmul at raft.py:31-33), fp32-accurate from three
+ * split-bf16 MFMA products (hi.hi + hi.lo + lo.hi), batched over `batch`:
+ *   out[b] (m x nc, row-major) = a[b] (m x k, row stride lda) . B[b]
+ *   layout 0: B = bm[b] given as k x nc (row stride ldb >= nc)       -> grad_fmap1 = P G
+ *   layout 1: B = bm[b]^T, bm[b] given as nc x k (row stride ldb >= k) -> dP = fmap1 G^T
+ * Batch strides are m*lda for a and (layout 0 ? k : nc)*ldb for bm; out is contiguous.  K may be
+ * split over workgroups: then `workspace` must hold rmd_corr_grad_gemm_workspace_bytes() bytes
+ * (0 = none needed) and a second pass sums the partial tiles in a fixed order (deterministic). */
+size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, int nc);
+int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m, int k, int nc,
+                       int layout, float* out, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);

@@ -1,0 +1,336 @@
+// corr_grad.hip — the two GEMMs of the RAFT correlation backward as split-bf16 (x3) MFMA GEMMs.
+//
+// Backward of raft.CorrBlock.__init__ (qzed/raft-meets-dicl src/models/impls/raft.py:31-47: corr =
+// fmap1^T fmap2 / sqrt(C), then avg_pool2d per level).  With the lookup backward's dense
+// query-minor gradient G (B, T, N) over the T pooled targets of all levels (corr_backward.hip) and
+// the pooled, scaled target features P (B, C, T), autograd of the matmul is
+//   dfmap1 = P . G           (B, C, N)   K = T        layout 0: G is K x Nc, n contiguous
+//   dP     = fmap1 . G^T     (B, C, T)   K = N        layout 1: G is Nc x K, k contiguous
+// (dP is then un-pooled onto dfmap2 by rmd_corr_unpool_targets).  Both run here in fp32 accuracy
+// as three bf16 MFMA products per k-step, x = hi + lo, hi = bf16(x), lo = bf16(x - hi):
+//   acc += A_lo.B_hi + A_hi.B_lo + A_hi.B_hi        (the dropped lo.lo term is ~2^-16 relative)
+// — the same split as the forward x3 GEMM (corr_pyramid_x3.hip) — instead of hipBLASLt's exact-f32
+// MFMA path (v_mfma_f32_32x32x2_f32 runs at 1/16 of the bf16 rate).
+//
+// Geometry: one workgroup (8 waves, 2 per SIMD) owns a 256 (M) x 128 (Nc) output tile; wave
+// (wm = w & 3, wn = w >> 2) owns 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16.  K runs in
+// 64-deep chunks: the next chunk's fp32 operands are loaded into registers while the MFMAs of the
+// current chunk run, then split into hi / lo and written to LDS (one 272-B row per operand row:
+// hi 128 B | lo 128 B | 16 B pad = 17 x 16 B, so the 8-lane groups of a ds_read_b128 hit 8
+// distinct 16-B bank slots).  K is split over `splits` workgroups when the tile grid alone does not
+// fill the 256 CUs; the partial tiles go to a workspace and a second kernel sums them in a fixed
+// order (deterministic, no atomics).
+
+#include "rmd_common.h"
+
+namespace rmd {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kTM = 256, kTN = 128, kKC = 64;
+constexpr int kRowB = 272;                                  // hi 128 B | lo 128 B | pad 16 B
+constexpr int kLdsA = kTM * kRowB, kLdsB = kTN * kRowB;     // 69,632 + 34,816 B
+
+struct GemmArgs {
+    const float* A;
+    const float* Bm;
+    float* out;                 // final output (splits == 1) or the split workspace
+    long long lda, ldb;         // row strides (elements)
+    long long sa, sb, so;       // batch strides (elements) of A, Bm, out
+    int M, K, Nc, batch;
+    int kper;                   // K per split (multiple of kKC)
+    int splits, ntm, ntn;
+};
+
+__device__ __forceinline__ void split4(float a, float b, float c, float d, bf16x4& hi, bf16x4& lo) {
+    hi[0] = (__bf16)a;
+    hi[1] = (__bf16)b;
+    hi[2] = (__bf16)c;
+    hi[3] = (__bf16)d;
+    lo[0] = (__bf16)(a - (float)hi[0]);
+    lo[1] = (__bf16)(b - (float)hi[1]);
+    lo[2] = (__bf16)(c - (float)hi[2]);
+    lo[3] = (__bf16)(d - (float)hi[3]);
+}
+
+// 4 consecutive elements of a row starting at column k (row valid, k < kend checked per element)
+template <bool VEC>
+__device__ __forceinline__ float4 load4(const float* __restrict__ row, int k, int kend) {
+    if (VEC && k + 3 < kend) return *reinterpret_cast<const float4*>(row + k);
+    float4 v;
+    v.x = k + 0 < kend ? row[k + 0] : 0.f;
+    v.y = k + 1 < kend ? row[k + 1] : 0.f;
+    v.z = k + 2 < kend ? row[k + 2] : 0.f;
+    v.w = k + 3 < kend ? row[k + 3] : 0.f;
+    return v;
+}
+
+// VA / VB: 16-B aligned rows (row stride % 4 == 0) -> float4 loads; LAYOUT 0 / 1 as above
+template <bool VA, bool VB, int LAYOUT>
+__global__ void __launch_bounds__(512, 1)
+grad_gemm_x3(GemmArgs p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* sA = smem;
+    unsigned char* sB = smem + kLdsA;
+    const int nwg = gridDim.x;
+    int id = xcd_block(blockIdx.x, nwg);       // consecutive ids (same batch, same A rows) share an XCD
+    const int tn = id % p.ntn;
+    id /= p.ntn;
+    const int tm = id % p.ntm;
+    id /= p.ntm;
+    const int split = id % p.splits;
+    const int b = id / p.splits;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w & 3, wn = w >> 2;
+    const int m0 = tm * kTM, n0 = tn * kTN;
+    const int kb = split * p.kper, ke = min(p.K, kb + p.kper);
+    const float* __restrict__ A = p.A + (size_t)b * p.sa;
+    const float* __restrict__ Bm = p.Bm + (size_t)b * p.sb;
+
+    float4 ra[8], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int row = m0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
+            ra[it] = row < p.M ? load4<VA>(A + (size_t)row * p.lda, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if constexpr (LAYOUT == 0) {
+            // thread (kq, nq): k rows 4kq..4kq+3 of columns 4nq..4nq+3 — lanes (kq & 3, nq) of a wave
+            // read 4 k rows x 256 contiguous bytes; waves 0-3 / 4-7 take column halves 0-63 / 64-127
+            const int kq = (lane & 3) | ((w & 3) << 2), n = n0 + 64 * (w >> 2) + 4 * (lane >> 2);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = k0 + 4 * kq + r;
+                rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (k < ke) {
+                    const float* src = Bm + (size_t)k * p.ldb;
+                    if (VB && n + 3 < p.Nc) {
+                        rb[r] = *reinterpret_cast<const float4*>(src + n);
+                    } else {
+                        rb[r].x = n + 0 < p.Nc ? src[n + 0] : 0.f;
+                        rb[r].y = n + 1 < p.Nc ? src[n + 1] : 0.f;
+                        rb[r].z = n + 2 < p.Nc ? src[n + 2] : 0.f;
+                        rb[r].w = n + 3 < p.Nc ? src[n + 3] : 0.f;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int row = n0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
+                rb[it] = row < p.Nc ? load4<VB>(Bm + (size_t)row * p.ldb, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            bf16x4 hi, lo;
+            split4(ra[it].x, ra[it].y, ra[it].z, ra[it].w, hi, lo);
+            unsigned char* d = sA + (it * 32 + (tid >> 4)) * kRowB + (tid & 15) * 8;
+            *reinterpret_cast<bf16x4*>(d) = hi;
+            *reinterpret_cast<bf16x4*>(d + 128) = lo;
+        }
+        if constexpr (LAYOUT == 0) {
+            // transpose: column 4nq + j of the thread's 4 k rows -> LDS row of that column, k offset 4kq
+            const int kq = (lane & 3) | ((w & 3) << 2), nr = 64 * (w >> 2) + 4 * (lane >> 2);
+            const float c0[4] = {rb[0].x, rb[1].x, rb[2].x, rb[3].x};
+            const float c1[4] = {rb[0].y, rb[1].y, rb[2].y, rb[3].y};
+            const float c2[4] = {rb[0].z, rb[1].z, rb[2].z, rb[3].z};
+            const float c3[4] = {rb[0].w, rb[1].w, rb[2].w, rb[3].w};
+            const float* cols[4] = {c0, c1, c2, c3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bf16x4 hi, lo;
+                split4(cols[j][0], cols[j][1], cols[j][2], cols[j][3], hi, lo);
+                unsigned char* d = sB + (nr + j) * kRowB + kq * 8;
+                *reinterpret_cast<bf16x4*>(d) = hi;
+                *reinterpret_cast<bf16x4*>(d + 128) = lo;
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                bf16x4 hi, lo;
+                split4(rb[it].x, rb[it].y, rb[it].z, rb[it].w, hi, lo);
+                unsigned char* d = sB + (it * 32 + (tid >> 4)) * kRowB + (tid & 15) * 8;
+                *reinterpret_cast<bf16x4*>(d) = hi;
+                *reinterpret_cast<bf16x4*>(d + 128) = lo;
+            }
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+    const int j32 = lane & 31, h = lane >> 5;
+    const unsigned aoff = (unsigned)((wm * 64 + j32) * kRowB + h * 16);
+    const unsigned boff = (unsigned)((wn * 64 + j32) * kRowB + h * 16);
+
+    gload(kb);
+    for (int k0 = kb; k0 < ke; k0 += kKC) {
+        __syncthreads();                       // the previous chunk's fragment reads are done
+        lstore();
+        __syncthreads();
+        if (k0 + kKC < ke) gload(k0 + kKC);    // in flight during this chunk's MFMAs
+#pragma unroll
+        for (int s = 0; s < kKC / 16; ++s) {
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const unsigned char* pa = sA + aoff + i * 32 * kRowB + s * 32;
+                const unsigned char* pb = sB + boff + i * 32 * kRowB + s * 32;
+                ah[i] = *reinterpret_cast<const bf16x8*>(pa);
+                al[i] = *reinterpret_cast<const bf16x8*>(pa + 128);
+                bh[i] = *reinterpret_cast<const bf16x8*>(pb);
+                bl[i] = *reinterpret_cast<const bf16x8*>(pb + 128);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+                }
+        }
+    }
+
+    // C tile (32 x 32): lane (j32, h) holds rows 8 (v >> 2) + 4 h + (v & 3) of column j32
+    float* __restrict__ o = p.out + ((size_t)split * p.batch + b) * p.so;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + j32;
+            if (col >= p.Nc) continue;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int row = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+                if (row < p.M) o[(size_t)row * p.Nc + col] = acc[i][j][v];
+            }
+        }
+}
+
+// out[e] = sum_s ws[s][e] in split order (deterministic)
+__global__ void __launch_bounds__(256)
+grad_gemm_reduce(const float* __restrict__ ws, long long n, int splits, float* __restrict__ out) {
+    const long long i4 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if ((n & 3) == 0 && i4 + 3 < n) {
+        float4 s = *reinterpret_cast<const float4*>(ws + i4);
+        for (int k = 1; k < splits; ++k) {
+            const float4 v = *reinterpret_cast<const float4*>(ws + (size_t)k * n + i4);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        *reinterpret_cast<float4*>(out + i4) = s;
+    } else {
+        for (long long i = i4; i < n; ++i) {
+            float s = ws[i];
+            for (int k = 1; k < splits; ++k) s += ws[(size_t)k * n + i];
+            out[i] = s;
+        }
+    }
+}
+
+struct Plan {
+    int ntm, ntn, splits, kper;
+};
+
+// split count: smallest s minimising (workgroup rounds over 256 CUs) x (K chunks per split), plus a
+// small charge per split for the workspace pass
+Plan plan(int batch, int M, int K, int Nc) {
+    Plan pl{};
+    pl.ntm = (M + kTM - 1) / kTM;
+    pl.ntn = (Nc + kTN - 1) / kTN;
+    const long long tiles = (long long)pl.ntm * pl.ntn * batch;
+    const int nch = (K + kKC - 1) / kKC;
+    double best = 1e30;
+    pl.splits = 1;
+    for (int s = 1; s <= 8 && s <= nch; ++s) {
+        const long long rounds = (tiles * s + 255) / 256;
+        const int per = (nch + s - 1) / s;
+        const double cost = (double)rounds * per + (s > 1 ? 0.15 * s * (double)tiles / 256.0 : 0.0);
+        if (cost < best - 1e-9) {
+            best = cost;
+            pl.splits = s;
+        }
+    }
+    const int per = (nch + pl.splits - 1) / pl.splits;
+    pl.kper = per * kKC;
+    pl.splits = (nch + per - 1) / per;         // no empty split
+    return pl;
+}
+
+template <bool VA, bool VB, int LAYOUT>
+void launch_gemm(const GemmArgs& a, int nwg, hipStream_t st) {
+    auto k = grad_gemm_x3<VA, VB, LAYOUT>;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 kLdsA + kLdsB) == hipSuccess;
+    (void)attr;
+    k<<<nwg, 512, kLdsA + kLdsB, st>>>(a);
+}
+
+}  // namespace
+}  // namespace rmd
+
+extern "C" size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, int nc) {
+    if (batch <= 0 || m <= 0 || k <= 0 || nc <= 0) return 0;
+    const rmd::Plan pl = rmd::plan(batch, m, k, nc);
+    return pl.splits > 1 ? (size_t)pl.splits * batch * m * nc * sizeof(float) : 0;
+}
+
+extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m,
+                                  int k, int nc, int layout, float* out, void* workspace, void* stream) {
+    RMD_REQUIRE(a && bm && out, RMD_ERR_ARG, "rmd_corr_grad_gemm: null pointer");
+    RMD_REQUIRE(batch > 0 && m > 0 && k > 0 && nc > 0, RMD_ERR_SHAPE, "rmd_corr_grad_gemm: empty shape");
+    RMD_REQUIRE(layout == 0 || layout == 1, RMD_ERR_ARG, "rmd_corr_grad_gemm: layout must be 0 or 1");
+    RMD_REQUIRE(lda >= k && ldb >= (layout == 0 ? nc : k), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: bad row stride");
+    const rmd::Plan pl = rmd::plan(batch, m, k, nc);
+    RMD_REQUIRE(pl.splits == 1 || workspace, RMD_ERR_ARG, "rmd_corr_grad_gemm: workspace required (%d splits)",
+                pl.splits);
+    hipStream_t st = rmd::as_stream(stream);
+    rmd::GemmArgs g{};
+    g.A = a;
+    g.Bm = bm;
+    g.out = pl.splits > 1 ? static_cast<float*>(workspace) : out;
+    g.lda = lda;
+    g.ldb = ldb;
+    g.sa = (long long)m * lda;
+    g.sb = (layout == 0 ? (long long)k : (long long)nc) * ldb;
+    g.so = (long long)m * nc;
+    g.M = m;
+    g.K = k;
+    g.Nc = nc;
+    g.batch = batch;
+    g.kper = pl.kper;
+    g.splits = pl.splits;
+    g.ntm = pl.ntm;
+    g.ntn = pl.ntn;
+    const long long nwg = (long long)pl.ntm * pl.ntn * pl.splits * batch;
+    RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: grid too large");
+    const bool va = (lda & 3) == 0, vb = (ldb & 3) == 0;
+#define RMD_GG(VA, VB)                                                                      \
+    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, st) : rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, st))
+    if (va && vb) RMD_GG(true, true);
+    else if (va) RMD_GG(true, false);
+    else if (vb) RMD_GG(false, true);
+    else RMD_GG(false, false);
+#undef RMD_GG
+    int rc = rmd::check_launch("rmd_corr_grad_gemm");
+    if (rc != RMD_OK || pl.splits == 1) return rc;
+    const long long n = (long long)batch * m * nc;
+    const long long blocks = (n / 4 + 255) / 256 + 1;
+    rmd::grad_gemm_reduce<<<(unsigned)blocks, 256, 0, st>>>(static_cast<const float*>(workspace), n, pl.splits, out);
+    return rmd::check_launch("rmd_corr_grad_gemm reduce");
+}

@@ -203,8 +203,16 @@ class _CorrPyramidFn(torch.autograd.Function):
             _lib.check(lib.rmd_corr_pool_targets(_ptr(f2), b, c, h, w, levels, scale, _ptr(pooled), stream),
                        "rmd_corr_pool_targets")
             G = st.grad.view(b, t, n)
-            g1 = torch.bmm(pooled, G)                                       # (B, C, N)
-            dpool = torch.bmm(f1.view(b, c, n), G.transpose(1, 2))          # (B, C, T)
+            g1 = torch.empty((b, c, n), dtype=torch.float32, device=f1.device)
+            dpool = torch.empty((b, c, t), dtype=torch.float32, device=f1.device)
+            ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, c, t, n),
+                                 lib.rmd_corr_grad_gemm_workspace_bytes(b, c, n, t), 1),
+                             dtype=torch.uint8, device=f1.device)
+            # grad_fmap1 = P G (K = T), dP = fmap1 G^T (K = N): split-bf16 MFMA GEMMs (corr_grad.hip)
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 0, _ptr(g1), _ptr(ws),
+                                              stream), "rmd_corr_grad_gemm")
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 1, _ptr(dpool), _ptr(ws),
+                                              stream), "rmd_corr_grad_gemm")
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")
         st.grad = None

@@ -285,3 +285,30 @@ def test_dot_correlation_module_matches_reference_golden():
     with torch.no_grad():
         nodap = mod(_t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"]), dap=False)
     assert rel_max_err(nodap.cpu().numpy(), g["out_nodap"]) < 1e-4
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("b,m,k,nc", [(6, 256, 3790, 2852), (2, 100, 37, 45), (1, 300, 129, 130), (3, 32, 1000, 7)])
+def test_corr_grad_gemm_vs_fp64(layout, b, m, k, nc):
+    """rmd_corr_grad_gemm (split-bf16 x3 MFMA) against a float64 GEMM, elementwise.  Shapes: the cfg5
+    backward (B6, C256, T = 3790 pooled targets, N = 2852 queries; lda = 3790 is not 16-B aligned), ragged
+    tiles, M over two 256-row tiles, a K split into several workgroups."""
+    import ctypes
+    from rmd import _lib
+    g = torch.Generator(device="cpu").manual_seed(m + k)
+    a = torch.randn(b, m, k, generator=g)
+    bm = torch.randn(b, k, nc, generator=g) if layout == 0 else torch.randn(b, nc, k, generator=g)
+    ref = torch.bmm(a.double(), bm.double() if layout == 0 else bm.double().transpose(1, 2))
+    lib = _lib.lib()
+    ad, bd = a.to(DEV), bm.to(DEV)
+    out = torch.full((b, m, nc), float("nan"), device=DEV)
+    ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, m, k, nc), 1), dtype=torch.uint8, device=DEV)
+    rc = lib.rmd_corr_grad_gemm(ctypes.c_void_p(ad.data_ptr()), k, ctypes.c_void_p(bd.data_ptr()),
+                                nc if layout == 0 else k, b, m, k, nc, layout, ctypes.c_void_p(out.data_ptr()),
+                                ctypes.c_void_p(ws.data_ptr()), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = out.cpu().double()
+    # fp32-accurate: |err| <= 2e-5 * sqrt(k) * rms(|a||b|) — the dropped lo.lo term and fp32 accumulation
+    tol = 2e-5 * np.sqrt(k) + 1e-6
+    assert_close_elementwise(got.numpy(), ref.numpy(), rtol=1e-4, atol=tol)

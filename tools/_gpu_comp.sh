@@ -1,0 +1,13 @@
+# Component timings (HIP events) + RAFT correlation forward/backward at cfg5 under rocprofv3 stats.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${TAG:-comp}
+R=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $R
+timeout -k 10 400 python3 -u tools/bench_components.py 20 > $R/components.json 2> $R/components.err || exit 3
+timeout -k 10 200 python3 -u tools/bench_corr_bwd.py 10 fp32 > $R/corr_bwd_fp32.json 2> $R/corr_bwd.err || exit 4
+timeout -k 10 200 python3 -u tools/bench_corr_bwd.py 10 bf16 > $R/corr_bwd_bf16.json 2>> $R/corr_bwd.err || exit 5
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof_bwd -o run -- python3 tools/bench_corr_bwd.py 5 fp32 > $R/prof_bwd.log 2>&1 || exit 6
+find $R -name "*kernel_trace.csv" -delete
+echo done
