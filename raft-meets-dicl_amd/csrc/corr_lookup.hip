@@ -171,7 +171,7 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
         const int yc = min(max(yy, 0), lh - 1);
         const T* row_ptr = lvl + ((bq + yc) * txs) * chunk_stride + (long long)p * CW;
         float v[K];
-        if constexpr (ABL == 2) {
+        if constexpr (ABL >= 2) {
 #pragma unroll
             for (int k = 0; k < K; ++k) v[k] = fx * (float)k;
         } else {
@@ -184,7 +184,7 @@ __device__ __forceinline__ void lookup_level(const T* __restrict__ pyr, const Py
             const int bb = j - 1;
 #pragma unroll
             for (int a = 0; a < D; ++a) {
-                float* dst = o + (ABL == 1 ? 0 : (size_t)(a * D + bb) * N);
+                float* dst = o + ((ABL & 1) ? 0 : (size_t)(a * D + bb) * N);
                 const float val = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
                 if constexpr ((NT & 1) != 0) __builtin_nontemporal_store(val, dst);
                 else *dst = val;
@@ -218,6 +218,196 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
         default: lookup_level<T, R, 3, ABL, NT, PR>(pyr, g, b, pc, N, x, y, zmask, o, active, part); break;
     }
 }
+
+#ifdef RMD_DIAG
+// ---- v4 (diagnostic build, RMD_LOOKUP_V=4): all patch rows in flight, fewer instructions -------
+// Hypothesis tested: the product kernel waits for every patch row's loads (vmcnt(0), which on gfx9
+// also drains the previous row's 9 stores) before the next row's loads issue, and spends 46 % of its
+// wave cycles parked in s_waitcnt (profiles/lookup_pmc_r02.json).  This version
+//  * issues the loads of all PR+1 patch rows before any arithmetic or store (one round trip; the
+//    stores come after, so no store sits in front of a load's vmcnt);
+//  * folds the zero padding into per-lane weights computed once per (query, level) — a patch
+//    column is in the map or not for every row alike: wl[a] = (1-fx) in(a), wr[a] = fx in(a+1);
+//    row validity enters the two vertical weights of each output row — so each output costs one
+//    multiply + one fma per direction and no selects;
+//  * stores through a wave-uniform plane pointer + 32-bit lane offset (no 64-bit address math).
+// Same arithmetic as the reference up to rounding order.  Result (profiles/lookup_ab_r02.json):
+// 27.8 vs 23.8 us — 14 % fewer VALU instructions and one memory round trip per wave do not pay: the
+// product kernel moves 141 MB (counters) in 24 us = 5.9 TB/s, i.e. it is HBM-bound at ~94 % of the
+// 6.3 TB/s a streaming copy reaches, and more reads in flight per wave only cost occupancy (74 vs
+// 57 VGPRs).  Kept for re-measurement; not compiled into librmd.so.
+template <typename T, int R, int TW>
+__device__ __forceinline__ void fetch_row_words(const T* __restrict__ row_ptr, long long tile_stride, int tiles_x,
+                                                int tc0, unsigned (&wd)[((2 * R + 2 + 2 * TW - 2) / TW) * TW * sizeof(T) / 4]) {
+    constexpr int S = sizeof(T);
+    constexpr int EPW = 4 / S;
+    constexpr int K = 2 * R + 2;
+    constexpr int NC = (K + TW - 1 + TW - 1) / TW;
+    constexpr int CW = TW * S / 4;
+    // words shift_row_words can consume: the K kept elements after a shift of up to MAXW words (+1
+    // word for the odd half-word step) — the last chunk is loaded only that far, so no load result
+    // is dead (a dead load destination forces a vmcnt wait before its register is reused)
+    constexpr int MAXW = (TW - 1) * S / 4;
+    constexpr int NEED = (K - 1) / EPW + (S == 2 ? 1 : 0) + MAXW + 1;
+    constexpr int LW = NEED - (NC - 1) * CW;                               // 1 .. CW words
+    constexpr int LWP = LW <= 1 ? 1 : (LW <= 2 ? 2 : (LW <= 4 ? 4 : CW));
+    static_assert(LW >= 1 && LW <= CW, "chunk geometry");
+#pragma unroll
+    for (int c = 0; c < NC - 1; ++c) {
+        const int tc = min(max(tc0 + c, 0), tiles_x - 1);
+        unsigned tmp[CW];
+        load_words<CW, 0>(tmp, 0, reinterpret_cast<const unsigned char*>(row_ptr + (long long)tc * tile_stride));
+#pragma unroll
+        for (int i = 0; i < CW; ++i) wd[c * CW + i] = tmp[i];
+    }
+    {
+        const int tc = min(max(tc0 + NC - 1, 0), tiles_x - 1);
+        unsigned tmp[LWP];
+        load_words<LWP, 0>(tmp, 0, reinterpret_cast<const unsigned char*>(row_ptr + (long long)tc * tile_stride));
+#pragma unroll
+        for (int i = 0; i < CW; ++i) wd[(NC - 1) * CW + i] = i < LWP ? tmp[i < LWP ? i : 0] : 0u;
+    }
+}
+
+template <typename T, int R, int TW>
+__device__ __forceinline__ void shift_row_words(const unsigned (&wd0)[((2 * R + 2 + 2 * TW - 2) / TW) * TW * sizeof(T) / 4],
+                                                int sh, float (&v)[2 * R + 2]) {
+    constexpr int S = sizeof(T);
+    constexpr int EPW = 4 / S;
+    constexpr int K = 2 * R + 2;
+    constexpr int NW = ((K + 2 * TW - 2) / TW) * TW * S / 4;
+    constexpr int KW = (K + EPW - 1) / EPW + 1;
+    unsigned wd[NW + 1];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) wd[i] = wd0[i];
+    wd[NW] = 0u;
+    const int wsh = (sh * S) >> 2;
+    constexpr int MAXW = (TW - 1) * S / 4;
+#pragma unroll
+    for (int step = 1; step <= MAXW; step <<= 1) {
+        const bool on = (wsh & step) != 0;
+#pragma unroll
+        for (int i = 0; i < NW + 1; ++i) wd[i] = on ? ((i + step < NW + 1) ? wd[i + step] : 0u) : wd[i];
+    }
+    if constexpr (S == 2) {
+        const bool odd = (sh & 1) != 0;
+#pragma unroll
+        for (int i = 0; i < KW; ++i) wd[i] = odd ? __builtin_amdgcn_alignbyte(wd[i + 1], wd[i], 2) : wd[i];
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = word_elem<T>(wd[j / EPW], j % EPW);
+}
+
+template <typename T, int R, int L, int PR>
+__device__ __forceinline__ void lookup_level_v4(const T* __restrict__ pyr, const PyrGeom& g, int b, int p, int N,
+                                                float x, float y, unsigned zmask, float* __restrict__ slab,
+                                                bool active, int part) {
+    constexpr int D = 2 * R + 1;
+    constexpr int K = 2 * R + 2;
+    constexpr int KR = PR + 1;
+    constexpr int CW = level_chunk(L);
+    constexpr int NW = ((K + 2 * CW - 2) / CW) * CW * (int)sizeof(T) / 4;
+    const int lh = g.lh[L], lw = g.lw[L];
+    const int own0 = part * PR;
+    const int bb0 = min(own0, D - PR);
+    if (((zmask >> L) & 1u) || lh < 2 || lw < 2) {
+        // masked level -> 0; 1-pixel level -> NaN (the reference normalises by size-1 = 0, raft.py:73-74)
+        const float v = ((zmask >> L) & 1u) ? 0.f : __builtin_nanf("");
+        if (active)
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int r = 0; r < PR; ++r)
+                    if (own0 + r < D) __builtin_nontemporal_store(v, slab + (size_t)(a * D + own0 + r) * N + (unsigned)p);
+        return;
+    }
+    const float inv = 1.0f / (float)(1 << L);
+    const float rx = x * inv, ry = y * inv;
+    const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f), cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
+    const float fx0 = floorf(cx), fy0 = floorf(cy);
+    const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+
+    // ---- all patch rows' loads first ----
+    const T* lvl = pyr + g.off[L];
+    const long long chunk_stride = (long long)N * CW;
+    const long long bq = (long long)b * lh;
+    const int txs = g.tx[L];
+    const int tc0 = (xs >= 0) ? xs / CW : -((CW - 1 - xs) / CW);
+    const int sh = xs - tc0 * CW;
+    unsigned wd[KR][NW];
+#pragma unroll
+    for (int jj = 0; jj < KR; ++jj) {
+        const int yc = min(max(ys + bb0 + jj, 0), lh - 1);
+        fetch_row_words<T, R, CW>(lvl + ((bq + yc) * txs) * chunk_stride + (long long)p * CW, chunk_stride, txs, tc0,
+                                  wd[jj]);
+    }
+    __builtin_amdgcn_sched_barrier(0);      // keep every load of the patch ahead of the arithmetic
+
+    // weights from the unclamped coordinate: NaN / +-inf -> NaN window (tests/golden *_nonfinite)
+    const float fx = rx - floorf(rx), fy = ry - floorf(ry);
+    float wl[D], wr[D];
+    {
+        float in[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) in[j] = ((unsigned)(xs + j) < (unsigned)lw) ? 1.f : 0.f;
+#pragma unroll
+        for (int a = 0; a < D; ++a) {
+            wl[a] = (1.f - fx) * in[a];
+            wr[a] = fx * in[a + 1];
+        }
+    }
+
+    float hprev[D];
+    float okprev = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < KR; ++jj) {
+        const int j = bb0 + jj;
+        const float ok = ((unsigned)(ys + j) < (unsigned)lh) ? 1.f : 0.f;
+        float v[K];
+        shift_row_words<T, R, CW>(wd[jj], sh, v);
+        float hcur[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) hcur[a] = fmaf(wr[a], v[a + 1], wl[a] * v[a]);
+        if (jj > 0 && (PR == D || j - 1 >= own0)) {
+            const int bb = j - 1;
+            const float w0 = (1.f - fy) * okprev, w1 = fy * ok;
+            if (active)
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    float* plane = slab + (size_t)(a * D + bb) * N;                 // wave-uniform
+                    __builtin_nontemporal_store(fmaf(w1, hcur[a], w0 * hprev[a]), plane + (unsigned)p);
+                }
+        }
+#pragma unroll
+        for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
+        okprev = ok;
+    }
+}
+
+// grid: (query blocks, batch, level + levels * part)
+template <typename T, int R, int PR>
+__global__ void __launch_bounds__(kThreads)
+corr_lookup_v4_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
+                      float* __restrict__ out) {
+    constexpr int D = 2 * R + 1;
+    const int N = g.height * g.width;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    const int b = blockIdx.y;
+    const int L = (int)blockIdx.z % g.levels;
+    const int part = (int)blockIdx.z / g.levels;
+    const bool active = p < N;
+    const int pc = active ? p : N - 1;
+    const float x = coords[((size_t)b * 2 + 0) * N + pc];
+    const float y = coords[((size_t)b * 2 + 1) * N + pc];
+    float* slab = out + ((size_t)b * g.levels + L) * D * D * N;
+    switch (L) {
+        case 0: lookup_level_v4<T, R, 0, PR>(pyr, g, b, pc, N, x, y, zmask, slab, active, part); break;
+        case 1: lookup_level_v4<T, R, 1, PR>(pyr, g, b, pc, N, x, y, zmask, slab, active, part); break;
+        case 2: lookup_level_v4<T, R, 2, PR>(pyr, g, b, pc, N, x, y, zmask, slab, active, part); break;
+        default: lookup_level_v4<T, R, 3, PR>(pyr, g, b, pc, N, x, y, zmask, slab, active, part); break;
+    }
+}
+#endif  // RMD_DIAG
 
 // Row-exchange variant (diagnostic build, RMD_LOOKUP_XCH=1): one workgroup = 3 waves over the same 64
 // queries and level.  Wave w owns output rows [w*D/3, (w+1)*D/3) and loads only the patch rows no
@@ -353,8 +543,12 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
         const int nt = env_knob("RMD_LOOKUP_NT", 1);
         const int pr = env_knob("RMD_LOOKUP_SPLIT", 3);
         if constexpr (sizeof(T) == 2) {
-            if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
-            if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+            // ablations of the product kernel (3-way split, nt stores): 1 = no output traffic, 2 = no
+            // pyramid loads, 3 = neither (profiles/lookup_ablate_r02.json)
+            const dim3 g3(grid.x, grid.y, grid.z * 3);
+            if (radius == 4 && abl == 1) { corr_lookup_kernel<T, 4, 1, 1, 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+            if (radius == 4 && abl == 2) { corr_lookup_kernel<T, 4, 2, 1, 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
+            if (radius == 4 && abl == 3) { corr_lookup_kernel<T, 4, 3, 1, 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); return check_launch("rmd_corr_lookup"); }
         }
         if (radius == 4 && nt == 1 && pr != 3) {
             const dim3 gs(grid.x, grid.y, grid.z * ((9 + pr - 1) / pr));
@@ -389,11 +583,27 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
         return check_launch("rmd_corr_lookup");
     }
 #endif
+    const dim3 g3(grid.x, grid.y, grid.z * 3);
+#ifdef RMD_DIAG
+    // RMD_LOOKUP_V=4: all patch rows in flight + weight-folded padding (see lookup_level_v4)
+    if (env_knob("RMD_LOOKUP_V", 2) == 4) {
+        switch (radius) {
+#define RMD_CASE(RR) case RR: \
+            corr_lookup_v4_kernel<T, RR, (2 * RR + 3) / 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+            break;
+            RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
+#undef RMD_CASE
+            default:
+                set_error("rmd_corr_lookup: radius %d not in 1..8", radius);
+                return RMD_ERR_SHAPE;
+        }
+        return check_launch("rmd_corr_lookup");
+    }
+#endif
     // Product path: non-temporal output stores, and every radius splits a window's 2r+1 output rows
     // over 3 lanes (PR = floor((2r+3)/3) rows each, ceil((2r+1)/PR) = 3 for r = 1..8): with one lane
     // per (query, level) the cfg2 grid is 3.5 waves per SIMD that load, then store, in lock step; 3
     // parts give the memory system 10.5 waves whose read and write phases overlap.
-    const dim3 g3(grid.x, grid.y, grid.z * 3);
     switch (radius) {
 #define RMD_CASE(RR) case RR: \
         corr_lookup_kernel<T, RR, 0, 1, (2 * RR + 3) / 3><<<g3, kThreads, 0, st>>>(p, g, coords, zmask, out); \

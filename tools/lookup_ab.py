@@ -17,7 +17,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from rmd import ops  # noqa: E402
 
-KNOBS = ("XCH", "NT", "SPLIT")
+KNOBS = ("XCH", "NT", "SPLIT", "V")      # RMD_LOOKUP_<KNOB>; a name starting with RMD_ is set verbatim (RMD_ABLATE)
 
 
 def main():
@@ -27,13 +27,16 @@ def main():
     f1, f2, coords = bench.synthetic(8, 256, 55, 128, 12, 1234, dev)
     names = os.environ.get("RMD_AB", "XCH=1,XCH=0").split(",")
     pyr = ops.corr_pyramid(f1, f2, 4, precision)
+    if os.environ.get("LOOKUP_AB_SAME"):        # every lookup at iteration 6's coordinates (cache reuse bound)
+        coords = coords[6:7].expand(12, -1, -1, -1, -1).contiguous()
 
     def select(n):
         for k in KNOBS:
             os.environ.pop("RMD_LOOKUP_" + k, None)
+        os.environ.pop("RMD_ABLATE", None)
         for kv in filter(None, n.split("+")):
             k, v = kv.split("=")
-            os.environ["RMD_LOOKUP_" + k] = v
+            os.environ[k if k.startswith("RMD_") else "RMD_LOOKUP_" + k] = v
 
     select(names[0])
     ref = [ops.corr_lookup(pyr, coords[i], 4) for i in range(12)]
