@@ -1077,10 +1077,11 @@ dap_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, in
     }
 }
 
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
 // MFMA form (exact f32: v_mfma_f32_32x32x2_f32 == an fmaf chain): a workgroup owns 32 output
 // displacements x 128 pixels (4 waves x 32 pixels); its 32 rows of W (or of W^T) sit in LDS with an
 // odd row stride, x is read as two 128-B row segments per k-step.  grid (pixels/128, D/32, B).
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
 __global__ void __launch_bounds__(kThreads)
 dap_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
@@ -1126,6 +1127,124 @@ dap_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int 
         if (o < D) ob[(size_t)o * n] = acc[e];
     }
 }
+
+
+#ifdef RMD_DIAG
+#ifndef RMD_DAP_KC
+#define RMD_DAP_KC 8
+#endif
+// Blocked MFMA form: a workgroup (4 waves) owns an M-block of MT x 32 output displacements — all D
+// of them when D <= 128 — whose rows of W (or W^T) sit in LDS once, and its waves loop over 32-pixel
+// tiles; each x value is read from HBM once per M-block (once in all for D <= 128) and feeds MT
+// MFMAs.  The kernel is latency-bound, not bandwidth- or MFMA-bound (one round of ~2 waves per SIMD at
+// cfg4), so with KS > 0 (D <= 2 KS) a wave issues ALL of its tile's x loads (KS k-steps of 2 rows)
+// before the workgroup stages W and before any MFMA: one memory round trip per tile instead of one
+// per 8-row batch.  KS = 0 streams x in chunks of RMD_DAP_KC k-steps, two chunks in flight (large D).
+// x loads and out stores are buffer instructions on the batch slab (lane offset + scalar row
+// offset; rows >= D and pixels >= n fall outside the range: loads read 0, stores are dropped).
+// grid (workgroups per (M-block, batch), M-blocks, B).
+// Diagnostic build only (RMD_DAP_VALU=3): kernel time equals the round-1 form's at D = 81 (22.5 vs
+// 23.4 us), is slower at D = 49 (20.5 vs 17.2) and faster only for D = 324 with 4 tiles per wave
+// (240 vs 308 us) — profiles/dap_ab_r02.json.  The exact-f32 MFMA chain (64 cycles per
+// v_mfma_f32_32x32x2_f32) at ~2 waves per SIMD bounds every variant near 25 % of the f32 MFMA peak.
+template <int MT, int KS>
+__global__ void __launch_bounds__(kThreads)
+dap_mfma_blk_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
+                    float* __restrict__ out) {
+    extern __shared__ float sw[];                       // MT*32 rows x (Dk + 1)
+    const int Dk = (D + 1) & ~1, ld = Dk + 1;
+    const int o0 = blockIdx.y * 32 * MT, b = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 31, h = lane >> 5;
+    const int ntile = (n + 31) >> 5;
+    const float* xb0 = x + (size_t)b * D * n;
+    float* ob0 = out + (size_t)b * D * n;
+    auto rsrc = [&](const void* base) {
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
+                                                 (int)((unsigned)D * (unsigned)n * 4u), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t xr = rsrc(xb0);
+    const __amdgpu_buffer_rsrc_t orr = rsrc(ob0);
+    const unsigned rowb = (unsigned)n * 4u;              // bytes per displacement row
+    auto xoff = [&](int t, int k0) {                     // lane offset of rows 2 k0 + h, pixel of tile t
+        const int p = t * 32 + j;
+        return p < n ? (int)((unsigned)(2 * k0 + h) * rowb + (unsigned)p * 4u) : (int)0x80000000;
+    };
+    int t = blockIdx.x * 4 + w;
+    float xv[KS > 0 ? KS : 1];
+    if constexpr (KS > 0) {
+        const int vo = xoff(t < ntile ? t : 0, 0);
+#pragma unroll
+        for (int u = 0; u < KS; ++u)
+            xv[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
+    }
+    for (int k = threadIdx.x; k < 32 * MT * Dk; k += kThreads) {
+        const int r = k / Dk, i = k - r * Dk, o = o0 + r;
+        float v = 0.f;
+        if (o < D && i < D) v = transpose ? wgt[(size_t)i * D + o] : wgt[(size_t)o * D + i];
+        sw[r * ld + i] = v;
+    }
+    __syncthreads();
+    const int nks = Dk >> 1;                               // k-steps of 2 rows
+    for (bool first = true; t < ntile; t += gridDim.x * 4, first = false) {
+        f32x16_t acc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = f32x16_t{};
+        if constexpr (KS > 0) {
+            if (!first) {
+                const int vo = xoff(t, 0);
+#pragma unroll
+                for (int u = 0; u < KS; ++u)
+                    xv[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
+            }
+#pragma unroll
+            for (int u = 0; u < KS; ++u) {
+                if (u < nks) {
+                    const int kk = 2 * u + h;
+#pragma unroll
+                    for (int m = 0; m < MT; ++m)
+                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[(m * 32 + j) * ld + kk], xv[u], acc[m], 0, 0, 0);
+                }
+            }
+        } else {
+            constexpr int KC = RMD_DAP_KC;
+            float cur[KC], nxt[KC];
+            auto load_chunk = [&](float (&v)[KC], int c0) {
+                const int vo = xoff(t, c0);
+#pragma unroll
+                for (int u = 0; u < KC; ++u)
+                    v[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
+            };
+            load_chunk(cur, 0);
+            for (int c0 = 0; c0 < nks; c0 += KC) {
+                if (c0 + KC < nks) load_chunk(nxt, c0 + KC);
+#pragma unroll
+                for (int u = 0; u < KC; ++u) {
+                    if (c0 + u < nks) {
+                        const int kk = 2 * (c0 + u) + h;
+#pragma unroll
+                        for (int m = 0; m < MT; ++m)
+                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[(m * 32 + j) * ld + kk], cur[u], acc[m], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < KC; ++u) cur[u] = nxt[u];
+            }
+        }
+        // C tile: lane (j, h) holds rows 8 (e >> 2) + 4 h + (e & 3) of pixel column j
+        const int p = t * 32 + j;
+        const int so = p < n ? (int)((unsigned)(4 * h) * rowb + (unsigned)p * 4u) : (int)0x80000000;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[m][e]), orr, so,
+                                                      (int)((unsigned)(o0 + m * 32 + 8 * (e >> 2) + (e & 3)) * rowb), 0);
+    }
+}
+#endif  // RMD_DIAG
 
 int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int radius, int level, int nh, int nw,
                  int extra) {
@@ -1420,7 +1539,54 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
                        float* out, void* stream) {
     RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");
     RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap: bad sizes");
-    if (disp <= 1024 && !env_variant("RMD_DAP_VALU")) {
+#ifdef RMD_DIAG
+    if (disp <= 1024 && (size_t)disp * pixels * 4 < (1ull << 31) && env_variant("RMD_DAP_VALU") == 3) {
+        // blocked kernel: M-blocks of up to 4 MFMA row tiles (128 displacements), W block in LDS
+        // (the M-block shrinks until its W rows fit in 150 KB of LDS: D = 81 -> one block of 3 tiles,
+        // D = 324 -> 4 blocks of 3)
+        const int Dk = (disp + 1) & ~1;
+        const int mt_all = (disp + 31) / 32;
+        int mt = mt_all < 4 ? mt_all : 4;
+        while (mt > 1 && (size_t)32 * mt * (Dk + 1) * sizeof(float) > 150 * 1024) --mt;
+        const int mblocks = (mt_all + mt - 1) / mt;
+        const size_t lds = sizeof(float) * 32 * mt * (size_t)(Dk + 1);
+        const int ntile = (pixels + 31) / 32;
+        // workgroups per (M-block, batch): TPW pixel tiles per wave (diagnostic knob RMD_DAP_TPW, product 1),
+        // capped at ~8 workgroups per CU chip-wide
+        const int tpw = env_knob("RMD_DAP_TPW", 1);
+        int per = (ntile + 4 * tpw - 1) / (4 * tpw);
+        const int cap = (2048 + mblocks * batch - 1) / (mblocks * batch);
+        per = per < cap ? per : cap;
+        per = per < 1 ? 1 : per;
+        const dim3 grid(per, mblocks, batch);
+        hipStream_t st = as_stream(stream);
+        const int ks = Dk / 2 <= 32 ? 32 : (Dk / 2 <= 48 ? 48 : (Dk / 2 <= 64 ? 64 : 0));
+        const bool stream_x = env_variant("RMD_DAP_STREAM") != 0;     // diagnostic: force the KS = 0 form
+#define RMD_DAP(MT, KS)                                                                                     \
+        do {                                                                                                \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_blk_kernel<MT, KS>),          \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
+            dap_mfma_blk_kernel<MT, KS><<<grid, kThreads, lds, st>>>(x, weight, disp, pixels, transpose, out); \
+        } while (0)
+        if (ks == 32 && !stream_x) {
+            if (mt == 1) RMD_DAP(1, 32); else RMD_DAP(2, 32);
+        } else if (ks == 48 && !stream_x) {
+            if (mt == 2) RMD_DAP(2, 48); else RMD_DAP(3, 48);
+        } else if (ks == 64 && !stream_x) {
+            if (mt == 3) RMD_DAP(3, 64); else RMD_DAP(4, 64);
+        } else {
+            switch (mt) {
+                case 1: RMD_DAP(1, 0); break;
+                case 2: RMD_DAP(2, 0); break;
+                case 3: RMD_DAP(3, 0); break;
+                default: RMD_DAP(4, 0); break;
+            }
+        }
+#undef RMD_DAP
+        return check_launch("rmd_dap/mfma");
+    }
+#endif
+    if (disp <= 1024 && env_variant("RMD_DAP_VALU") == 0) {
         const int Dk = (disp + 1) & ~1;
         const size_t lds = sizeof(float) * 32 * (size_t)(Dk + 1);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_kernel),
