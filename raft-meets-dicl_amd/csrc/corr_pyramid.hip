@@ -672,6 +672,8 @@ struct Lvl {
     unsigned cs;      // chunk stride (bytes)
     unsigned cw2;     // chunk bytes (per query)
     int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
+    unsigned hd;      // paired block (corr_pyramid_w8): added to the offsets of the block's second row
+                      // half, which holds the NEXT column block's rows: -(half rows) * rs + chunks * cs
 };
 
 struct Ctx {
@@ -700,7 +702,8 @@ struct LaneOff {
 __device__ __forceinline__ LaneOff lane_offsets(const Ctx& c, int q, int h, bool live) {
     LaneOff r;
 #pragma unroll
-    for (int l = 0; l < 4; ++l) r.o[l] = live ? (unsigned)q * c.l[l].cw2 + (unsigned)h * c.l[l].rs : kBig;
+    for (int l = 0; l < 4; ++l)
+        r.o[l] = live ? (unsigned)q * c.l[l].cw2 + (unsigned)h * (c.l[l].rs + (l == 3 ? c.l[3].hd : 0u)) : kBig;
     return r;
 }
 
@@ -740,6 +743,7 @@ __device__ __forceinline__ Ctx ctx_qtm(const PyrGeom& g, int b, int qt, int rb, 
         c.l[l].cs = __builtin_amdgcn_readfirstlane(32u * cw * 2u);
         c.l[l].cw2 = (unsigned)cw * 2u;
         c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+        c.l[l].hd = 0u;
     }
     return c;
 }
@@ -757,7 +761,8 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         swp(x0, y0);
         swp(x1, y1);
         const i32x4 d = {(int)x0, (int)x1, (int)y0, (int)y1};
-        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[0].rsrc, (int)(lo.o[0] + soff(c.l[0], 2 * m, tc)), 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[0].rsrc,
+                                               (int)(lo.o[0] + soff(c.l[0], 2 * m, tc) + (m >= 4 ? c.l[0].hd : 0u)), 0, AUX);
     }
     // level-1 sums of level-1 row m, col group tc: cols {2h, 2h+1} (tc 0) / {4+2h, 5+2h} (tc 1)
 #pragma unroll
@@ -774,7 +779,8 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         swp(x0, y0);
         swp(x1, y1);
         const i32x4 d = {(int)x0, (int)y0, (int)x1, (int)y1};
-        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[1].rsrc, (int)(lo.o[1] + soff(c.l[1], 2 * p, 0)), 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(d, c.l[1].rsrc,
+                                               (int)(lo.o[1] + soff(c.l[1], 2 * p, 0) + (p >= 2 ? c.l[1].hd : 0u)), 0, AUX);
         // level-2 sums of level-2 row p: lane h holds cols {h, 2+h}
 #pragma unroll
         for (int cg = 0; cg < 2; ++cg)
@@ -787,7 +793,8 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         unsigned y = pk(0.0625f * st.s2[2 * k + 1][0], 0.0625f * st.s2[2 * k + 1][1]);  // row 2k+1: cols h, 2+h
         swp(x, y);          // lane h now holds row 2k+h: x = cols {0,2}, y = cols {1,3}
         const i32x2 d = {(int)__builtin_amdgcn_perm(y, x, 0x05040100u), (int)__builtin_amdgcn_perm(y, x, 0x07060302u)};
-        __builtin_amdgcn_raw_buffer_store_b64(d, c.l[2].rsrc, (int)(lo.o[2] + soff(c.l[2], 2 * k, 0)), 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(d, c.l[2].rsrc,
+                                              (int)(lo.o[2] + soff(c.l[2], 2 * k, 0) + (k >= 1 ? c.l[2].hd : 0u)), 0, AUX);
     }
     if constexpr (S == 15) {
         // level 3: rows 0, 1 (level-2 rows 0-1 / 2-3), cols 0, 1 (level-2 cols {0,1} / {2,3});
@@ -940,6 +947,7 @@ corr_pyramid_pipe(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB
         c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
         c.l[l].cw2 = (unsigned)cw * 2u;
         c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+        c.l[l].hd = 0u;
     }
 
     // ---- this wave's query tiles: t_k = first + k * stride, k < n -------------------------------
@@ -1127,26 +1135,59 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx
     }
 }
 
+// Balanced schedule (host: w8_balance; product PP kernel only).
+//  * pair: the last block row has at most 8 valid target rows and W % 32 == 0, so two horizontally
+//    adjacent last-row blocks share one workgroup: rows 0-7 of its virtual 16x16 block are block
+//    cb's rows, rows 8-15 block cb+1's (A staging and the stores' second-half delta Lvl::hd follow),
+//    and no workgroup spends half its MFMAs on rows past the map (cfg2: 55 = 3 x 16 + 7).
+//  * helpers: with fewer primary workgroups (one per block x batch) than CUs, every primary stops
+//    after qfull query tiles and one helper per primary, dispatched after all primaries (so it lands
+//    on a CU with no primary), re-stages that block's A and runs tiles [qfull, nqt).
+struct Bal {
+    int pair;        // last block row paired
+    int nprim;       // primary workgroups (blocks x batch x qsplit)
+    int qfull;       // query tiles of a primary when helpers exist (== nqt otherwise)
+    int helpers;     // 1: one helper per primary
+};
+
 }  // namespace w8
 
 template <int AUX, bool ROLL, bool PAD = true, bool RING = false, bool PP = false, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
-                __half* __restrict__ pyr, int drop_stores, int stagger) {
+                __half* __restrict__ pyr, int drop_stores, int stagger, w8::Bal bal) {
     constexpr int Cp = 256, CPR = Cp / 8, WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int H = g.height, W = g.width, N = H * W;
     const int ncb = (W + 15) >> 4;
-    const int nblk = ((H + 15) >> 4) * ncb;
-    const int nwg = gridDim.x;
+    const int nrb = (H + 15) >> 4;
+    // blocks per image: full blocks, then (pair) the last row's blocks two per workgroup
+    const int nfull = bal.pair ? (nrb - 1) * ncb : nrb * ncb;
+    const int nblk = nfull + (bal.pair ? ncb / 2 : 0);
     const int orig = blockIdx.x;
-    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
-    const int tb = lid % nblk;
+    int lid, q_lo = 0, q_hi = (N + 31) >> 5;
+    if (orig < bal.nprim) {
+        // primaries: XCD-aware remap over the primary range (XCD k runs the k-th eighth)
+        const int nwg = bal.nprim;
+        const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+        lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+        if (bal.helpers) q_hi = bal.qfull;
+    } else {
+        // helpers: the same logical id as their primary, placed by blockIdx.x - nprim; nprim is a
+        // multiple of 8 when helpers exist, so a helper lands on its primary's XCD (its batch's L2)
+        const int hid = orig - bal.nprim;
+        const int nwg = bal.nprim;
+        const int xcd = hid & 7, qq = nwg >> 3, rr = nwg & 7;
+        lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (hid >> 3);
+        q_lo = bal.qfull;
+    }
+    const int ib = lid % nblk;
     const int rest = lid / nblk;
     const int split = rest % qsplit;
     const int b = rest / qsplit;
+    const bool paired = ib >= nfull;
+    const int tb = paired ? (nrb - 1) * ncb + 2 * (ib - nfull) : ib;
     const int rb = tb / ncb, cb = tb - rb * ncb;
     const int ty0 = rb * 16, tx0 = cb * 16;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1156,7 +1197,9 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
     const __bf16* gA = opA + (size_t)b * N * Cp;
     for (int id = tid; id < 256 * CPR; id += 64 * WAVES) {
         const int row = id / CPR, c = id - row * CPR;
-        const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
+        // virtual row y >= 8 of a paired block = row y - 8 of the next column block
+        const bool second = paired && (row >> 4) >= 8;
+        const int ty = ty0 + (row >> 4) - (second ? 8 : 0), tx = tx0 + (row & 15) + (second ? 16 : 0);
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
         if constexpr (PAD)
@@ -1196,6 +1239,7 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
         c.l[l].cw2 = (unsigned)cw * 2u;
         c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+        c.l[l].hd = paired ? __builtin_amdgcn_readfirstlane(nch * (unsigned)N * cw * 2u - (unsigned)(span / 2) * rs) : 0u;
     }
 
     const int nqt = (N + 31) >> 5;
@@ -1209,9 +1253,11 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         // while its partner owns the matrix pipe (free-running partners drift into lock step: PMC of
         // the free-running kernel shows VALU co-issued with MFMA in only a third of its VALU cycles).
         // Waves 4-7 start one phase late; every wave runs 2 * nmax + 1 barriers.
-        const int f0 = split * WAVES;
-        const int nmax = f0 < nqt ? (nqt - f0 + stride - 1) / stride : 0;
-        const int nw = qt < nqt ? (nqt - qt + stride - 1) / stride : 0;
+        // this workgroup's query tiles: [q_lo, q_hi) (all of them unless helpers split the block)
+        const int f0 = q_lo + split * WAVES;
+        qt = f0 + w;
+        const int nmax = f0 < q_hi ? (q_hi - f0 + stride - 1) / stride : 0;
+        const int nw = qt < q_hi ? (q_hi - qt + stride - 1) / stride : 0;
         const bool late = w >= 4;
         unsigned b0 = pb0, b1 = pb1;
         asm volatile("" : "+v"(b0), "+v"(b1));
@@ -1370,6 +1416,58 @@ int launch_prepare(const float* f1, const float* f2, int C, float scale, const r
     return check_launch("rmd_corr_prepare");
 }
 
+// Balanced schedule of the w8 GEMM (w8::Bal).  Costs in rounds (one query tile per wave, 8 per
+// workgroup): a primary with all tiles takes ceil(nqt/8); with helpers it takes ceil(qfull/8) and
+// the CUs left without a primary run ceil(nprim / spare) helpers of ceil((nqt-qfull)/8) + 0.2
+// rounds (the A re-staging).  qfull (a multiple of 8) minimises the larger of the two; helpers are
+// used only if that beats ceil(nqt/8).  Diagnostic knob RMD_W8_BAL: 0 off, 1 (product) pairing only,
+// 2 pairing + helpers.  Measured at cfg2 (profiles/gemm_ab_r02_bal.json): 0.2280 / 0.2257 / 0.2271 ms,
+// all bitwise identical — removing the 12.5 % of MFMA tiles that fall past the map and evening out
+// the per-CU work does not move the kernel: it is bound by the chip-wide pyramid write stream
+// (1.05 GB at 4.6-5.1 TB/s), not by any CU's share.  Pairing stays (the same time for 12.5 % fewer
+// MFMAs, 224 instead of 256 workgroups); helpers are off.
+w8::Bal w8_balance(const rmd_pyramid_desc& d, int qs, bool pp_kernel) {
+    const int N = d.height * d.width;
+    const int nqt = (N + 31) / 32;
+    const int nrb = (d.height + 15) / 16, ncb = (d.width + 15) / 16;
+    const int rows_last = d.height - 16 * (nrb - 1);
+    const int mode = pp_kernel ? env_knob("RMD_W8_BAL", 1) : 0;
+    w8::Bal bal{0, nrb * ncb * d.batch * qs, nqt, 0};
+    if (mode == 0 || qs != 1) return bal;
+    if (nrb >= 2 && rows_last <= 8 && d.width % 32 == 0) {
+        bal.pair = 1;
+        bal.nprim = ((nrb - 1) * ncb + ncb / 2) * d.batch;
+    }
+    if (mode < 2) return bal;
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            ncu = n;
+        if (ncu <= 0) ncu = 256;
+    }
+    const int spare = ncu - bal.nprim;
+    if (spare <= 0 || bal.nprim % 8 != 0) return bal;
+    const int per = (bal.nprim + spare - 1) / spare;               // helpers per spare CU
+    double best = (double)((nqt + 7) / 8);
+    int qbest = nqt;
+    for (int qf = 8; qf < nqt; qf += 8) {
+        const double tp = (double)((qf + 7) / 8);
+        const double th = per * ((double)((nqt - qf + 7) / 8) + 0.2);
+        const double t = tp > th ? tp : th;
+        if (t < best - 0.25) {
+            best = t;
+            qbest = qf;
+        }
+    }
+    if (qbest < nqt) {
+        bal.helpers = 1;
+        bal.qfull = qbest;
+    }
+    return bal;
+}
+
 template <bool F32, typename TOut>
 int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid, void* workspace, hipStream_t st) {
     using T = typename Operand<F32>::T;
@@ -1418,8 +1516,13 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                 drop = env_knob("RMD_ABLATE", 0) == 1 || env_knob("RMD_ABLATE", 0) == 3;
                 stagger = env_knob("RMD_W8_STAGGER", 0);
 #endif
+                bool pp_kernel = true;
+#ifdef RMD_DIAG
+                pp_kernel = env_knob("RMD_W8_PAD", 1) != 0 && env_knob("RMD_W8_RING", 2) == 2;
+#endif
+                const w8::Bal bal = w8_balance(d, qs, pp_kernel);
                 (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds_w8);
-                kern<<<nblk * d.batch * qs, 512, lds_w8, st>>>(opA, opB, geom, qs, out, drop, stagger);
+                kern<<<bal.nprim * (bal.helpers ? 2 : 1), 512, lds_w8, st>>>(opA, opB, geom, qs, out, drop, stagger, bal);
                 return check_launch("rmd_corr_pyramid/gemm-w8");
             }
 #ifdef RMD_DIAG

@@ -312,3 +312,28 @@ def test_corr_grad_gemm_vs_fp64(layout, b, m, k, nc):
     # fp32-accurate: |err| <= 2e-5 * sqrt(k) * rms(|a||b|) — the dropped lo.lo term and fp32 accumulation
     tol = 2e-5 * np.sqrt(k) + 1e-6
     assert_close_elementwise(got.numpy(), ref.numpy(), rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("b,h,w", [(1, 55, 128), (2, 40, 64), (1, 23, 96), (3, 55, 128), (1, 46, 62)])
+def test_w8_balanced_schedule_levels_vs_oracle(b, h, w):
+    """The bf16 GEMM's balanced schedule (corr_pyramid.hip w8_balance): a last block row of <= 8 target
+    rows is paired two blocks per workgroup (55 = 3*16 + 7; 40 = 2*16 + 8 also stores a level-3 row
+    from the pair's second half), and helper workgroups run the query tiles past qfull.  Every level
+    of sampled queries (including the last query tiles, which the helpers write) against the oracle;
+    (1, 23, 96) has an odd number of column blocks, (1, 46, 62) neither pairs nor splits."""
+    import rmd
+    rng = np.random.default_rng(h * w + b)
+    c = 256
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    pyr = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "bf16")
+    n = h * w
+    sel = np.unique(np.concatenate([rng.choice(n, 96, replace=False), np.arange(max(0, n - 40), n),
+                                    np.arange(0, 8)]))
+    ref = oracle.corr_pyramid(f1.reshape(b, c, n)[:, :, sel][:, :, None, :].astype(np.float64),
+                              f2.astype(np.float64), 4)
+    torch.cuda.synchronize()
+    for i in range(4):
+        got = pyr.unpack(i).cpu().numpy().reshape(b, n, *ref[i].shape[-2:])[:, sel]
+        r = ref[i].reshape(b, len(sel), *ref[i].shape[-2:])
+        assert rel_max_err(got, r) < 1e-2, f"level {i}"

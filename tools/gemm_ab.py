@@ -41,6 +41,8 @@ def main():
         os.environ["RMD_W8_RING"] = "1" if "ring" in knobs else ("0" if "plain" in knobs or "nopad" in knobs else "2")
         stag = int(knobs.split("stag")[1].split("+")[0]) if "stag" in knobs else 0
         os.environ["RMD_W8_STAGGER"] = str(stag + (1000 if "prio" in knobs else 0))     # "w8+prio" = s_setprio 1 on waves 4-7
+        # "w8+bal0" / "w8+bal2" = balanced schedule off / pairing + helpers (default 1: pairing only)
+        os.environ["RMD_W8_BAL"] = "0" if "bal0" in knobs else ("2" if "bal2" in knobs else "1")
         os.environ["RMD_GEMM_KERNEL"] = kern
         os.environ["RMD_ABLATE"] = abl or "0"
         os.environ["RMD_STORE_AUX"] = aux or "2"
