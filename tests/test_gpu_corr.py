@@ -337,3 +337,28 @@ def test_w8_balanced_schedule_levels_vs_oracle(b, h, w):
         got = pyr.unpack(i).cpu().numpy().reshape(b, n, *ref[i].shape[-2:])[:, sel]
         r = ref[i].reshape(b, len(sel), *ref[i].shape[-2:])
         assert rel_max_err(got, r) < 1e-2, f"level {i}"
+
+
+@pytest.mark.parametrize("precision,c,b,h,w", [("bf16", 200, 2, 23, 40), ("bf16", 193, 1, 17, 33),
+                                               ("fp32", 200, 2, 23, 40), ("fp32", 96, 3, 9, 70),
+                                               ("fp32", 256, 1, 8, 8)])
+def test_gemm_paths_odd_shapes_vs_oracle(precision, c, b, h, w):
+    """Channel counts that zero-pad to the w8 kernel's 256 (bf16: C = 193, 200) or run the x3 kernel
+    below 256 (fp32: C = 96, 200), ragged maps (23x40, 17x33, 9x70 -> level 3 of 1 row) and a map of one
+    8x8 block: full pyramid of every query against the oracle."""
+    import rmd
+    from rmd import _lib
+    lib = _lib.lib()
+    compute = _lib.RMD_BF16 if precision == "bf16" else _lib.RMD_BF16X3
+    storage = _lib.RMD_F16 if precision == "bf16" else _lib.RMD_F32
+    kern = lib.rmd_corr_gemm_kernel(_lib.describe(b, h, w, 4, storage), c, compute)
+    assert kern == (b"w8" if precision == "bf16" else b"x3")
+    rng = np.random.default_rng(c * h + w)
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    pyr = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, precision)
+    ref = oracle.corr_pyramid(f1.astype(np.float64), f2.astype(np.float64), 4)
+    torch.cuda.synchronize()
+    for i in range(4):
+        got = pyr.unpack(i).cpu().numpy().reshape(ref[i].shape)
+        assert rel_max_err(got, ref[i]) < TOL[precision], f"level {i}"
