@@ -1507,7 +1507,14 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                     if (env_knob("RMD_ABLATE", 0) == 4) kern = corr_pyramid_w8<2, false, true, true, true, 4>;
                     else if (env_knob("RMD_ABLATE", 0) == 5) kern = corr_pyramid_w8<2, false, true, true, true, 5>;
                     else if (env_knob("RMD_ABLATE", 0) >= 2) kern = corr_pyramid_w8<2, false, true, true, true, 2>;
-                    else if (aux != 2) kern = corr_pyramid_w8<0, false, true, true, true>;
+                    else if (aux == 0) kern = corr_pyramid_w8<0, false, true, true, true>;
+                    // cache-policy A/B of the pyramid stores (gfx950 cpol bits: 1 sc0, 2 nt, 16 sc1)
+                    else if (aux == 1) kern = corr_pyramid_w8<1, false, true, true, true>;
+                    else if (aux == 3) kern = corr_pyramid_w8<3, false, true, true, true>;
+                    else if (aux == 16) kern = corr_pyramid_w8<16, false, true, true, true>;
+                    else if (aux == 17) kern = corr_pyramid_w8<17, false, true, true, true>;
+                    else if (aux == 18) kern = corr_pyramid_w8<18, false, true, true, true>;
+                    else if (aux == 19) kern = corr_pyramid_w8<19, false, true, true, true>;
                 } else if (env_knob("RMD_W8_RING", 2) == 1) {
                     kern = corr_pyramid_w8<2, false, true, true>;
                 } else {
