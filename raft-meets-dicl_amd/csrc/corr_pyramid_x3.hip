@@ -264,130 +264,144 @@ __device__ __forceinline__ void ksteps(f32x16 (&acc)[4], bf16x8 (&acur)[8], bf16
     }
 }
 
+// Persistent schedule: the work is cut into units = (image, quarter of the query tiles, target block)
+// — `quarters` tile ranges of tq tiles per block — and workgroup lid (one per CU) runs units lid,
+// lid + nwg, lid + 2 nwg, ...  Ordered image-major, then quarter, then block, a time slot of nwg
+// consecutive units keeps each XCD's workgroups on one or two (image, quarter) tile ranges, whose
+// B fragments (55 tiles x 32 KB = 1.8 MB at cfg2) then stay in that XCD's L2.  At cfg2, 448
+// one-block workgroups take 2 rounds on 256 CUs (the second 3/4 full); 1792 quarter units take 7
+// even slots.  Each unit re-stages its block's A (128 KB) — quarters = 1 and nwg = units is the
+// one-block-per-workgroup launch.
+//
 // ABL (diagnostic build only): 1 = drop every store (descriptor range 0), 2 = no k-loop (epilogue only)
 template <bool PP, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
-                const __bf16* __restrict__ bLo, PyrGeom g, int qsplit, float* __restrict__ pyr) {
+                const __bf16* __restrict__ bLo, PyrGeom g, int units, int quarters, int tq,
+                float* __restrict__ pyr) {
     constexpr int WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = g.height, W = g.width, N = H * W;
     const int ncb = (W + kBlockCols - 1) / kBlockCols;
     const int nblk = ((H + kBlockRows - 1) / kBlockRows) * ncb;
-    const int lid = xcd_block(blockIdx.x, gridDim.x);
-    const int tb = lid % nblk;
-    const int rest = lid / nblk;
-    const int split_ = rest % qsplit;
-    const int b = rest / qsplit;
-    const int rb = tb / ncb, cb = tb - rb * ncb;
-    const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
+    const int nqt = (N + 31) >> 5;
+    const int nwg = gridDim.x;
+    const int lid = xcd_block(blockIdx.x, nwg);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j = lane & 31, h = lane >> 5;
 
-    // ---- A block (hi and lo) -> LDS, zero rows for targets outside the image --------------------
-    const size_t abase = (size_t)b * N * 256;
-    for (int id = tid; id < kBlockRows * kBlockCols * 64; id += 64 * WAVES) {
-        const int row = id >> 6, c = id & 63;                 // c < 32: hi chunk c, else lo chunk c - 32
-        const int y = row >> 4, x = row & 15;
-        const int ty = ty0 + y, tx = tx0 + x;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        const __bf16* src = c < 32 ? aHi : aLo;
-        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
-        *reinterpret_cast<uint4*>(smem + (size_t)lds_row(y, x) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v;
-    }
-    __syncthreads();
+    for (int u = lid; u < units; u += nwg) {            // uniform per workgroup
+        const int per_img = nblk * quarters;
+        const int b = u / per_img;
+        const int r = u - b * per_img;
+        const int qd = r / nblk;
+        const int tb = r - qd * nblk;
+        const int t_lo = qd * tq, t_hi = min(nqt, t_lo + tq);
+        const int rb = tb / ncb, cb = tb - rb * ncb;
+        const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
 
-    // ---- per-level store descriptors of this block (wave-uniform) -------------------------------
-    Lvl L[4];
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-        const int span = kBlockRows >> l, nch = l == 0 ? 2 : 1;
-        const int y0 = rb * span, xc0 = cb * nch;
-        const bool lv = l < g.levels;
-        const int cw = g.tw[l];
-        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
-        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 4u : 0u;
-        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-        float* bp = pyr + base;
-        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
-        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
-        L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
-                                                      (int)__builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs),
-                                                      0x00020000);
-        L[l].rs = __builtin_amdgcn_readfirstlane(rs);
-        L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
-        L[l].rows = __builtin_amdgcn_readfirstlane(rows);
-        L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
-    }
-
-    // A fragment of tile ti = 2 rg + cg, k-step s, half p: base[cg] + rg*32*kRow + 32 s + 512 p
-    unsigned b0 = (unsigned)j * kRow + 16u * h, b1 = b0 + 64u * kRow;
-    asm volatile("" : "+v"(b0), "+v"(b1));
-
-    const int nqt = (N + 31) >> 5;
-    const size_t bb = ((size_t)b * nqt * 1024 + lane) * 8;
-    const int stride = WAVES * qsplit;
-    int qt = split_ * WAVES + w;
-    if constexpr (!PP) {
-        if (qt >= nqt) return;
-    }
-    // B fragments stream through an 8-slot register ring: k-step s of a tile lives in slot s % 8 and is
-    // loaded at k-step s - 7 (the previous tile's k-steps 9-15 load this tile's 0-6), 7 k-steps
-    // (84 MFMAs) ahead; A fragments of k-step s + 1 are read from LDS at the top of k-step s.  Each
-    // k-step is one scheduling region, so neither set of loads drifts to just before its MFMAs.
-    const __bf16* pb = bHi + bb + (size_t)qt * 8192;
-    const __bf16* pbl = bLo + bb + (size_t)qt * 8192;
-    bf16x8 rh[kRing], rl[kRing];
-    if (qt < nqt) {
-#pragma unroll
-        for (int s = 0; s < kRing - 1; ++s) {
-            rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
-            rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
+        // ---- A block (hi and lo) -> LDS, zero rows for targets outside the image ----------------
+        __syncthreads();                                // the previous unit's fragment reads are done
+        const size_t abase = (size_t)b * N * 256;
+        for (int id = tid; id < kBlockRows * kBlockCols * 64; id += 64 * WAVES) {
+            const int row = id >> 6, c = id & 63;                 // c < 32: hi chunk c, else lo chunk c - 32
+            const int y = row >> 4, x = row & 15;
+            const int ty = ty0 + y, tx = tx0 + x;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            const __bf16* src = c < 32 ? aHi : aLo;
+            if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
+            *reinterpret_cast<uint4*>(smem + (size_t)lds_row(y, x) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v;
         }
-    }
-    if constexpr (PP) {
-        // ping-pong phases (as corr_pyramid_w8): waves w and w + 4 of each SIMD alternate between the
-        // MFMA phase and the epilogue phase, separated by workgroup barriers; 2 * nmax + 1 per wave
-        const int f0 = split_ * WAVES;
-        const int nmax = f0 < nqt ? (nqt - f0 + stride - 1) / stride : 0;
-        const int nw = qt < nqt ? (nqt - qt + stride - 1) / stride : 0;
-        const bool late = w >= 4;
-        if (late) __builtin_amdgcn_s_barrier();
-        for (int k = 0; k < nmax; ++k) {
-            f32x16 acc[4];
-            const int qn = qt + stride;
-            if (k < nw && ABL == 2) {
+        __syncthreads();
+
+        // ---- per-level store descriptors of this block (wave-uniform) ---------------------------
+        Lvl L[4];
 #pragma unroll
-                for (int ti = 0; ti < 4; ++ti)
+        for (int l = 0; l < 4; ++l) {
+            const int span = kBlockRows >> l, nch = l == 0 ? 2 : 1;
+            const int y0 = rb * span, xc0 = cb * nch;
+            const bool lv = l < g.levels;
+            const int cw = g.tw[l];
+            const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+            const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 4u : 0u;
+            const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
+            float* bp = pyr + base;
+            const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+            const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+            L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+                                                          (int)__builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs),
+                                                          0x00020000);
+            L[l].rs = __builtin_amdgcn_readfirstlane(rs);
+            L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
+            L[l].rows = __builtin_amdgcn_readfirstlane(rows);
+            L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+        }
+
+        // A fragment of tile ti = 2 rg + cg, k-step s, half p: base[cg] + rg*32*kRow + 32 s + 512 p
+        unsigned b0 = (unsigned)j * kRow + 16u * h, b1 = b0 + 64u * kRow;
+        asm volatile("" : "+v"(b0), "+v"(b1));
+
+        const size_t bb = ((size_t)b * nqt * 1024 + lane) * 8;
+        const int stride = WAVES;
+        int qt = t_lo + w;
+        // B fragments stream through an 8-slot register ring: k-step s of a tile lives in slot s % 8
+        // and is loaded at k-step s - 7 (the previous tile's k-steps 9-15 load this tile's 0-6), 7
+        // k-steps (84 MFMAs) ahead; A fragments of k-step s + 1 are read from LDS at the top of k-step
+        // s.  Each k-step is one scheduling region, so neither set of loads drifts to just before its
+        // MFMAs.
+        bf16x8 rh[kRing], rl[kRing];
+        if (qt < t_hi) {
+            const __bf16* pb = bHi + bb + (size_t)qt * 8192;
+            const __bf16* pbl = bLo + bb + (size_t)qt * 8192;
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
-            } else if (k < nw) {
+            for (int s = 0; s < kRing - 1; ++s) {
+                rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
+                rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
+            }
+        }
+        if constexpr (PP) {
+            // ping-pong phases (as corr_pyramid_w8): waves w and w + 4 of each SIMD alternate between
+            // the MFMA phase and the epilogue phase, separated by workgroup barriers; 2 nmax + 1 per
+            // wave and unit
+            const int nmax = t_lo < t_hi ? (t_hi - t_lo + stride - 1) / stride : 0;
+            const int nw = qt < t_hi ? (t_hi - qt + stride - 1) / stride : 0;
+            const bool late = w >= 4;
+            if (late) __builtin_amdgcn_s_barrier();
+            for (int k = 0; k < nmax; ++k) {
+                f32x16 acc[4];
+                const int qn = qt + stride;
+                if (k < nw && ABL == 2) {
+#pragma unroll
+                    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
+                } else if (k < nw) {
+                    const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+                    bf16x8 a0[8], a1[8];
+                    read_a<0>(a0, smem, b0, b1);
+                    ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192,
+                              bLo + bb + (size_t)qt * 8192, bHi + bb + pn, bLo + bb + pn);
+                }
+                __builtin_amdgcn_s_barrier();
+                if (k < nw) epilogue(acc, L, min(qt * 32 + j, N - 1), h);
+                __builtin_amdgcn_s_barrier();
+                qt = qn;
+            }
+            if (!late) __builtin_amdgcn_s_barrier();
+        } else {
+            while (qt < t_hi) {
+                f32x16 acc[4];
+                const int qn = qt + stride;
                 const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
                 bf16x8 a0[8], a1[8];
                 read_a<0>(a0, smem, b0, b1);
                 ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192, bLo + bb + (size_t)qt * 8192,
                           bHi + bb + pn, bLo + bb + pn);
+                epilogue(acc, L, min(qt * 32 + j, N - 1), h);
+                qt = qn;
             }
-            __builtin_amdgcn_s_barrier();
-            if (k < nw) epilogue(acc, L, min(qt * 32 + j, N - 1), h);
-            __builtin_amdgcn_s_barrier();
-            qt = qn;
         }
-        if (!late) __builtin_amdgcn_s_barrier();
-        return;
-    }
-    while (true) {
-        f32x16 acc[4];
-        const int qn = qt + stride;
-        const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
-        bf16x8 a0[8], a1[8];
-        read_a<0>(a0, smem, b0, b1);
-        ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192, bLo + bb + (size_t)qt * 8192,
-                  bHi + bb + pn, bLo + bb + pn);
-        epilogue(acc, L, min(qt * 32 + j, N - 1), h);
-        if (qn >= nqt) break;
-        qt = qn;
     }
 }
 
@@ -427,9 +441,37 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const __bf16* bHi = aLo + (size_t)d.batch * N * 256;
     const __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
     const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
-    int qs = 1;
-    while (nblk * d.batch * qs < 256 && qs * 16 <= nqt) qs *= 2;
-    qs = env_knob("RMD_X3_QS", qs);
+    // schedule (see corr_pyramid_x3): quarters Q in {1, 2, 4, 8} minimising slots x rounds per unit,
+    // slots = ceil(B nblk Q / CUs) (one 137-KB-LDS workgroup per CU), rounds = ceil(nqt / Q / 8); a
+    // unit re-stages A, charged as 0.3 round.  Q = 1 with one workgroup per unit is the plain launch
+    // (the only one when the grid is already several CU-loads deep).
+    static int ncu = 0;
+    if (ncu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            ncu = n;
+        if (ncu <= 0) ncu = 256;
+    }
+    int quarters = 1;
+    double best = 1e30;
+    // product: Q = 1.  Measured at cfg2 (profiles/x3_ab_r02_persist.json), bitwise identical:
+    // Q = 1 0.632 ms, Q <= 2 0.619, Q = 4 (7 even slots) 0.627 — like the w8 GEMM, the kernel is
+    // bound chip-wide (2.09 GB fp32 pyramid stream + the MFMA phases' overlap), not by CU balance
+    const int qmax = env_knob("RMD_X3_QMAX", 1);
+    for (int q = 1; q <= qmax && q * 8 <= nqt; q *= 2) {
+        const long long units = (long long)nblk * d.batch * q;
+        const int tq = (nqt + q - 1) / q;
+        const double slots = (double)((units + ncu - 1) / ncu);
+        const double cost = slots * ((tq + 7) / 8 + 0.3);
+        if (cost < best - 1e-9) {
+            best = cost;
+            quarters = q;
+        }
+    }
+    const int tq = (nqt + quarters - 1) / quarters;
+    const long long units = (long long)nblk * d.batch * quarters;
+    const int nwg = (int)(units < ncu ? units : (quarters == 1 ? units : ncu));
     const int lds = kBlockRows * kBlockCols * kRow;
     // product: ping-pong phases; the diagnostic build's RMD_X3_PP=0 runs free-running waves (A/B)
 #ifdef RMD_DIAG
@@ -440,7 +482,7 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     auto kern = corr_pyramid_x3<true>;
 #endif
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    kern<<<nblk * d.batch * qs, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), qs, reinterpret_cast<float*>(pyr));
+    kern<<<nwg, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), (int)units, quarters, tq, reinterpret_cast<float*>(pyr));
     return check_launch("rmd_corr_pyramid/gemm-x3");
 }
 

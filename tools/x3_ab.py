@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of the fp32-mode (split-bf16, x3) correlation GEMM at cfg2 (diagnostic build).
-RMD_X3_PP=1 (ping-pong phases, product) vs 0 (free-running waves); HIP events around the GEMM launch."""
+RMD_X3_PP=1 (ping-pong phases, product) vs 0 (free-running waves); RMD_X3_QMAX = largest number of
+query-tile quarters the persistent schedule may use (1 = one workgroup per block, the round-2 launch);
+HIP events around the GEMM launch."""
 import json
 import os
 import sys
@@ -17,11 +19,11 @@ from rmd import ops  # noqa: E402
 dev = torch.device("cuda", 0)
 f1, f2, _ = bench.synthetic(8, 256, 55, 128, 1, 1234, dev)
 res, ref = {}, None
-VARIANTS = {"1": ("1", "0", "1"), "0": ("0", "0", "1"), "pp_nostore": ("1", "1", "1"), "pp_epilogue_only": ("1", "2", "1"),
-            "qs2": ("1", "0", "2"), "qs4": ("1", "0", "4"), "qs4_nostore": ("1", "1", "4")}
+VARIANTS = {"1": ("1", "0", "8"), "0": ("0", "0", "8"), "pp_nostore": ("1", "1", "8"), "pp_epilogue_only": ("1", "2", "8"),
+            "q1": ("1", "0", "1"), "q1_nostore": ("1", "1", "1"), "q2": ("1", "0", "2")}
 for rnd in range(4):
     for v, (pp, abl, qs) in VARIANTS.items():
-        os.environ["RMD_X3_QS"] = qs
+        os.environ["RMD_X3_QMAX"] = qs
         os.environ["RMD_X3_PP"] = pp
         os.environ["RMD_ABLATE"] = abl
         ev = []
@@ -37,5 +39,5 @@ for rnd in range(4):
             res["mismatch_" + v] = int((pyr.data != ref).sum())
 out = {k: (sorted(v)[len(v) // 2] if isinstance(v, list) else v) for k, v in res.items()}
 print(json.dumps({"pp_median_ms": out["1"], "free_median_ms": out["0"], "pp_nostore_ms": out["pp_nostore"],
-                  "pp_epilogue_only_ms": out["pp_epilogue_only"], "qs2_ms": out["qs2"], "qs4_ms": out["qs4"],
-                  "qs4_nostore_ms": out["qs4_nostore"], **{k: v for k, v in out.items() if k.startswith("mis")}}))
+                  "pp_epilogue_only_ms": out["pp_epilogue_only"], "q1_ms": out["q1"], "q1_nostore_ms": out["q1_nostore"],
+                  "q2_ms": out["q2"], **{k: v for k, v in out.items() if k.startswith("mis")}}))
