@@ -29,7 +29,10 @@ namespace {
 constexpr int kThreads = 256;                        // prepare kernels
 constexpr int kLookThreads = 256, kWaves = kLookThreads / 64;
 constexpr int kBX = 16, kBY = 2, kQ = kBX * kBY;     // query block = 2 query segments
-constexpr int kMaxT = 384;                           // targets of one band
+#ifndef RMD_OTF_MAXT
+#define RMD_OTF_MAXT 384
+#endif
+constexpr int kMaxT = RMD_OTF_MAXT;                  // targets of one band
 constexpr int kLd = kMaxT + 5;                       // S row stride (spreads queries over banks)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
