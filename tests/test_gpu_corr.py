@@ -362,3 +362,28 @@ def test_gemm_paths_odd_shapes_vs_oracle(precision, c, b, h, w):
     for i in range(4):
         got = pyr.unpack(i).cpu().numpy().reshape(ref[i].shape)
         assert rel_max_err(got, ref[i]) < TOL[precision], f"level {i}"
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_large_batch_offsets_vs_oracle(precision):
+    """B = 40 at the cfg2 map (pyramid 5.2 GB fp16 / 10.4 GB fp32, lookup output 365 MB): the last images' level
+    offsets run far past 2^32 bytes, so any 32-bit batch arithmetic in the GEMM epilogue or the lookup
+    would land in the wrong image.  Sampled queries of the first and the last image vs the oracle."""
+    import rmd
+    b, c, h, w = 40, 256, 55, 128
+    g = torch.Generator(device="cpu").manual_seed(5)
+    f1 = torch.randn(b, c, h, w, generator=g)
+    f2 = torch.randn(b, c, h, w, generator=g)
+    ys, xs = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32), indexing="ij")
+    co = torch.stack([xs, ys])[None] + 3.0 * torch.randn(b, 2, h, w, generator=g)
+    cb = rmd.raft.CorrBlock(f1.to(DEV), f2.to(DEV), 4, 4, precision=precision)
+    out = cb(co.to(DEV))
+    rng = np.random.default_rng(9)
+    n = h * w
+    sel = np.sort(rng.choice(n, 64, replace=False))
+    for bi in (0, b - 1):
+        got = out[bi].reshape(324, n)[:, torch.from_numpy(sel).to(DEV)].cpu().numpy()
+        f1s = f1[bi:bi + 1].reshape(1, c, n)[:, :, sel][:, :, None, :].double().numpy()
+        cos = co[bi:bi + 1].reshape(1, 2, n)[:, :, sel][:, :, None, :].double().numpy()
+        ref = oracle.corr_lookup(oracle.corr_pyramid(f1s, f2[bi:bi + 1].double().numpy(), 4), cos, 4)
+        assert rel_max_err(got, ref.reshape(324, -1)) < TOL[precision], f"image {bi}"
