@@ -1094,6 +1094,7 @@ __device__ __forceinline__ void mma_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16]
 // tile's k-steps 9-15 load this tile's 0-6 — instead of all 16 (64 VGPRs) being held for the whole
 // tile; the 32 VGPRs freed double-buffer the A fragments: k-step s+1's 8 fragments are read at the
 // top of k-step s.  One scheduling region per k-step keeps both sets of loads where they are issued.
+constexpr int kEpiStores = 24;  // buffer stores of one ping-pong epilogue (23 in the .s), for vmcnt_pad_n
 constexpr int kRing = 8;
 
 template <int S>
@@ -1152,7 +1153,9 @@ struct Bal {
 
 }  // namespace w8
 
-template <int AUX, bool ROLL, bool PAD = true, bool RING = false, bool PP = false, int ABL = 0>
+// VPAD (ping-pong kernel): one branch per phase pair + vmcnt_pad_n after the ring prologue (product;
+// the diagnostic build's RMD_W8_VPAD=0 compiles the previous form for A/B)
+template <int AUX, bool ROLL, bool PAD = true, bool RING = false, bool PP = false, int ABL = 0, bool VPAD = true>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
                 __half* __restrict__ pyr, int drop_stores, int stagger, w8::Bal bal) {
@@ -1266,11 +1269,41 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
 #pragma unroll
             for (int s = 0; s < w8::kRing - 1; ++s) ring[s] = *reinterpret_cast<const bf16x8*>(gB + (size_t)qt * 8192 + 512 * s);
         }
+        if constexpr (VPAD) vmcnt_pad_n<w8::kEpiStores>(pyr);
         if (late) __builtin_amdgcn_s_barrier();
         for (int k = 0; k < nmax; ++k) {
             f32x16 acc[8];
             const int qn = qt + stride;
-            if (k < nw) {
+            if (VPAD && k < nw) {
+                // both phases in one wave-uniform branch: every path that loads ring fragments issues
+                // the epilogue stores after them (vmcnt_pad_n, rmd_common.h)
+                if constexpr (ABL == 2 || ABL == 4) {
+#pragma unroll
+                    for (int ti = 0; ti < 8; ++ti)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
+                } else {
+                    bf16x8 a0[8], a1[8];
+                    w8::read_a8<0>(a0, smem, b0, b1);
+                    w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
+                                       gB + (size_t)min(qn, nqt - 1) * 8192);
+                }
+                __builtin_amdgcn_s_barrier();
+                if constexpr (ABL >= 4) {
+                    const pipe::Ctx ct = pipe::ctx_qtm(g, b, qt, rb, cb, pyr);
+                    const pipe::LaneOff lo = pipe::lane_offsets(ct, j, h, true);
+                    pipe::EpiState st;
+                    w8::epilogue<0, AUX>(acc, ct, lo, st);
+                } else {
+                    const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+                    pipe::EpiState st;
+                    w8::epilogue<0, AUX>(acc, c, lo, st);
+                }
+                __builtin_amdgcn_s_barrier();
+                qt = qn;
+                continue;
+            }
+            if (!VPAD && k < nw) {
                 if constexpr (ABL == 2 || ABL == 4) {       // diagnostic: no k-loop (epilogue-only timing)
 #pragma unroll
                     for (int ti = 0; ti < 8; ++ti)
@@ -1284,7 +1317,7 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
                 }
             }
             __builtin_amdgcn_s_barrier();
-            if (k < nw) {
+            if (!VPAD && k < nw) {
                 if constexpr (ABL >= 4) {       // diagnostic: query-tile-major store layout (timing only)
                     const pipe::Ctx ct = pipe::ctx_qtm(g, b, qt, rb, cb, pyr);
                     const pipe::LaneOff lo = pipe::lane_offsets(ct, j, h, true);
@@ -1515,6 +1548,8 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
                     else if (aux == 17) kern = corr_pyramid_w8<17, false, true, true, true>;
                     else if (aux == 18) kern = corr_pyramid_w8<18, false, true, true, true>;
                     else if (aux == 19) kern = corr_pyramid_w8<19, false, true, true, true>;
+                    if (env_knob("RMD_W8_VPAD", 1) == 0 && env_knob("RMD_ABLATE", 0) == 0 && aux == 2)
+                        kern = corr_pyramid_w8<2, false, true, true, true, 0, false>;
                 } else if (env_knob("RMD_W8_RING", 2) == 1) {
                     kern = corr_pyramid_w8<2, false, true, true>;
                 } else {

@@ -219,6 +219,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
     }
 }
 
+constexpr int kEpiStores = 24;  // buffer stores of one epilogue (23 in the .s), for vmcnt_pad_n
 constexpr int kRing = 8;     // B ring slots (16 % kRing == 0: k-step s of every tile maps to slot s % kRing)
 
 // A fragments (hi in [2ti], lo in [2ti+1]) of k-step S for the 4 target tiles
@@ -274,7 +275,8 @@ __device__ __forceinline__ void ksteps(f32x16 (&acc)[4], bf16x8 (&acur)[8], bf16
 // one-block-per-workgroup launch.
 //
 // ABL (diagnostic build only): 1 = drop every store (descriptor range 0), 2 = no k-loop (epilogue only)
-template <bool PP, int ABL = 0>
+// PAD: vmcnt_pad after the ring prologue (product; the diagnostic build's RMD_X3_PAD=0 drops it for A/B)
+template <bool PP, int ABL = 0, bool PAD = true>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
                 const __bf16* __restrict__ bLo, PyrGeom g, int units, int quarters, int tq,
@@ -360,6 +362,7 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
                 rl[s] = *reinterpret_cast<const bf16x8*>(pbl + 512 * s);
             }
         }
+        if constexpr (PAD) vmcnt_pad_n<kEpiStores>(pyr);
         if constexpr (PP) {
             // ping-pong phases (as corr_pyramid_w8): waves w and w + 4 of each SIMD alternate between
             // the MFMA phase and the epilogue phase, separated by workgroup barriers; 2 nmax + 1 per
@@ -369,23 +372,30 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
             const bool late = w >= 4;
             if (late) __builtin_amdgcn_s_barrier();
             for (int k = 0; k < nmax; ++k) {
-                f32x16 acc[4];
                 const int qn = qt + stride;
-                if (k < nw && ABL == 2) {
+                // one wave-uniform branch holds both phases, so every path that loads ring fragments
+                // also issues the epilogue stores after them (see vmcnt_pad_n)
+                if (k < nw) {
+                    f32x16 acc[4];
+                    if constexpr (ABL == 2) {
 #pragma unroll
-                    for (int ti = 0; ti < 4; ++ti)
+                        for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
-                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
-                } else if (k < nw) {
-                    const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
-                    bf16x8 a0[8], a1[8];
-                    read_a<0>(a0, smem, b0, b1);
-                    ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192,
-                              bLo + bb + (size_t)qt * 8192, bHi + bb + pn, bLo + bb + pn);
+                            for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
+                    } else {
+                        const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+                        bf16x8 a0[8], a1[8];
+                        read_a<0>(a0, smem, b0, b1);
+                        ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192,
+                                  bLo + bb + (size_t)qt * 8192, bHi + bb + pn, bLo + bb + pn);
+                    }
+                    __builtin_amdgcn_s_barrier();
+                    epilogue(acc, L, min(qt * 32 + j, N - 1), h);
+                    __builtin_amdgcn_s_barrier();
+                } else {
+                    __builtin_amdgcn_s_barrier();
+                    __builtin_amdgcn_s_barrier();
                 }
-                __builtin_amdgcn_s_barrier();
-                if (k < nw) epilogue(acc, L, min(qt * 32 + j, N - 1), h);
-                __builtin_amdgcn_s_barrier();
                 qt = qn;
             }
             if (!late) __builtin_amdgcn_s_barrier();
@@ -476,6 +486,7 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     // product: ping-pong phases; the diagnostic build's RMD_X3_PP=0 runs free-running waves (A/B)
 #ifdef RMD_DIAG
     auto kern = env_knob("RMD_X3_PP", 1) ? corr_pyramid_x3<true> : corr_pyramid_x3<false>;
+    if (env_knob("RMD_X3_PAD", 1) == 0) kern = corr_pyramid_x3<true, 0, false>;
     if (env_knob("RMD_ABLATE", 0) == 1) kern = corr_pyramid_x3<true, 1>;
     if (env_knob("RMD_ABLATE", 0) == 2) kern = corr_pyramid_x3<true, 2>;
 #else

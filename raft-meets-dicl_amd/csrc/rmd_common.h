@@ -95,6 +95,21 @@ constexpr int env_variant(const char*) { return 0; }
 constexpr int env_knob(const char*, int dflt) { return dflt; }
 #endif
 
+// vmcnt on gfx950 (as on every gfx9-family CU) is ONE in-order counter for vector loads AND stores.
+// The GEMM tile loops load the next tile's first B fragments (a register ring) before the current
+// tile's epilogue stores; the compiler's wait before a ring register's first use must then leave the
+// stores issued after that load outstanding.  But at the loop header it merges the back-edge state
+// with the preheader's — where nothing follows the prologue loads — and keeps the smaller distance:
+// vmcnt(ring) instead of vmcnt(ring + stores), so every tile's first MFMAs also wait for the write
+// acknowledgements of the previous epilogue.  NPAD stores into a zero-range buffer (dropped by the
+// range check: no memory traffic) after the prologue loads give the preheader path the same distance.
+template <int NPAD>
+__device__ __forceinline__ void vmcnt_pad_n(void* base) {
+    const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NPAD; ++i) __builtin_amdgcn_raw_buffer_store_b32(0, nul, 64 * i, 0, 0);   // 64-B apart: not merged
+}
+
 __device__ __forceinline__ float to_f32(float v) { return v; }
 __device__ __forceinline__ float to_f32(__half v) { return __half2float(v); }
 
