@@ -1078,7 +1078,171 @@ dap_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, in
 }
 
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 dbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 dbf16x4_t;
 
+// ---- DAP as a split-bf16 (x3) MFMA GEMM (product form) -----------------------------------------
+// out_b (D x n) = W (D x D) . x_b (D x n), fp32 accuracy from three bf16 products per k-step,
+// v = hi + lo, hi = bf16(v), lo = bf16(v - hi):  acc += W_lo.x_hi + W_hi.x_lo + W_hi.x_hi  (the
+// dropped lo.lo term is ~2^-16 relative; same split as the fp32-mode correlation GEMM).  The exact
+// f32 MFMA (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate and held the round-1 kernel at
+// ~25 % of even that peak (0.27 ms at D = 324); here the 3 bf16 products cost 3/16.
+// Geometry: a workgroup owns an M-block of MT x 32 output displacements (all of them when D <= 128)
+// and one chunk of the batch image's 32-pixel tiles.  The block's W rows (or W^T rows, transpose)
+// are split once into hi / lo bf16 in LDS — rows of 2 Kp + 16 bytes, an odd number of 16-B slots,
+// so a ds_read_b128 lane group hits distinct bank slots; each wave then sweeps its tiles: x is read
+// straight from HBM as the MFMA B operand (lane (r, h) holds rows 8h..8h+7 of k-step s at pixel r:
+// eight coalesced 128-B row segments), split in registers, KC k-steps per chunk with the next chunk
+// (or the next tile's first) in flight during the current chunk's MFMAs.  Rows >= D and pixels >= n
+// fall outside the per-image buffer range (loads read 0, stores are dropped).  The M-blocks of one
+// pixel chunk are consecutive workgroup ids (one XCD), so x is fetched from HBM once for all blocks.
+// Measured (profiles/dap_ab_r02.json, b8): D = 49 11.5 us, D = 81 13.1 us, D = 324 62 us, vs 16.8 /
+// 23.2 / 317 us for the exact-f32 MFMA form; error vs float64 1.5e-5 max-normalised.  At D = 324 the
+// MFMA floor is ~19 us and the HBM floor ~27 us: the two waves per SIMD wait on each chunk's x loads
+// (one chunk of prefetch distance in registers); staging x through LDS asynchronously is the next step.
+constexpr int kDapKC = 8;     // k-steps per x chunk (double-buffered)
+constexpr int kDapSG = 4;     // W staging: 4-element groups per thread in flight
+
+__device__ __forceinline__ void dap_split8(const float* v, dbf16x8_t& hi, dbf16x8_t& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = (__bf16)v[j];
+        lo[j] = (__bf16)(v[j] - (float)hi[j]);
+    }
+}
+
+template <int MT, int NW>
+__global__ void __launch_bounds__(NW * 64, 2)
+dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
+              int mblocks, int per, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+    const int Kp = (D + 15) & ~15, nks = Kp >> 4;
+    const int RB = 2 * Kp + 16;
+    unsigned char* const sh = sm;                       // hi rows
+    unsigned char* const sl = sm + MT * 32 * RB;        // lo rows
+    int id = xcd_block(blockIdx.x, gridDim.x);
+    const int mb = id % mblocks;
+    id /= mblocks;
+    const int pc = id % per, b = id / per;
+    const int o0 = mb * 32 * MT;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int ntile = (n + 31) >> 5;
+    auto rsrc = [&](const void* base) {
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
+                                                 (int)((unsigned)D * (unsigned)n * 4u), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t xr = rsrc(x + (size_t)b * D * n);
+    const __amdgpu_buffer_rsrc_t orr = rsrc(out + (size_t)b * D * n);
+    const unsigned rowb = (unsigned)n * 4u;
+    const unsigned aoff = (unsigned)(r * RB + 16 * h);
+    const int nch = (nks + kDapKC - 1) / kDapKC;
+
+    float xc[kDapKC * 8], xn[kDapKC * 8];
+    // chunk c of tile tt: rows 16 (KC c + u) + 8 h + j at pixel 32 tt + r (out of range past n / D)
+    auto load = [&](float (&v)[kDapKC * 8], int tt, int c) {
+        const int p = tt * 32 + r;
+        const unsigned base = p < n ? (unsigned)(8 * h + 16 * kDapKC * c) * rowb + (unsigned)p * 4u : 0x80000000u;
+#pragma unroll
+        for (int u = 0; u < kDapKC; ++u)
+            if (kDapKC * c + u < nks)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    v[u * 8 + j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        xr, (int)(base + (unsigned)(16 * u + j) * rowb), 0, 0));
+    };
+
+    int t = pc * NW + w;
+    const int tstride = per * NW;
+    if (t < ntile) load(xc, t, 0);          // in flight while the workgroup stages W
+
+    // stage the block's W rows as hi / lo bf16 (4 consecutive k per thread; W^T reads run along o),
+    // kDapSG groups' loads in flight per thread before any is converted
+    {
+        constexpr int rows = MT * 32;
+        const int kq = Kp >> 2, total = rows * kq;
+        for (int e0 = tid; e0 < total; e0 += NW * 64 * kDapSG) {
+            float v[kDapSG][4];
+            int ro[kDapSG];
+#pragma unroll
+            for (int g = 0; g < kDapSG; ++g) {
+                const int e = e0 + g * NW * 64;
+                int rr, k;
+                if (transpose) { rr = e % rows; k = 4 * (e / rows); }
+                else { rr = e / kq; k = 4 * (e - rr * kq); }
+                const int o = o0 + rr;
+                ro[g] = e < total ? rr * RB + 2 * k : -1;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int i = k + q;
+                    v[g][q] = (e < total && o < D && i < D) ? (transpose ? wgt[(size_t)i * D + o] : wgt[(size_t)o * D + i])
+                                                            : 0.f;
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < kDapSG; ++g) {
+                if (ro[g] < 0) continue;
+                dbf16x4_t hi, lo;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    hi[q] = (__bf16)v[g][q];
+                    lo[q] = (__bf16)(v[g][q] - (float)hi[q]);
+                }
+                *reinterpret_cast<dbf16x4_t*>(sh + ro[g]) = hi;
+                *reinterpret_cast<dbf16x4_t*>(sl + ro[g]) = lo;
+            }
+        }
+    }
+    __syncthreads();
+
+    while (t < ntile) {
+        f32x16_t acc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = f32x16_t{};
+        for (int c = 0; c < nch; ++c) {
+            int tn = t, cn = c + 1;
+            if (cn == nch) { tn = t + tstride; cn = 0; }
+            if (tn < ntile) load(xn, tn, cn);
+#pragma unroll
+            for (int u = 0; u < kDapKC; ++u) {
+                const int s = c * kDapKC + u;
+                if (s < nks) {
+                    dbf16x8_t bh, bl;
+                    dap_split8(xc + u * 8, bh, bl);
+#pragma unroll
+                    for (int m = 0; m < MT; ++m) {
+                        const unsigned a = aoff + (unsigned)(m * 32 * RB + 32 * s);
+                        const dbf16x8_t ah = *reinterpret_cast<const dbf16x8_t*>(sh + a);
+                        const dbf16x8_t al = *reinterpret_cast<const dbf16x8_t*>(sl + a);
+                        f32x16_t cacc = acc[m];
+                        cacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, cacc, 0, 0, 0);
+                        cacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, cacc, 0, 0, 0);
+                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, cacc, 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kDapKC * 8; ++q) xc[q] = xn[q];
+        }
+        // C tile: lane (r, h) holds rows 8 (e >> 2) + 4 h + (e & 3) of pixel column r
+        const int p = t * 32 + r;
+        const unsigned so = p < n ? (unsigned)(4 * h) * rowb + (unsigned)p * 4u : 0x80000000u;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const unsigned row = (unsigned)(o0 + m * 32 + 8 * (e >> 2) + (e & 3));
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[m][e]), orr, (int)(so + row * rowb), 0, 0);
+            }
+        t += tstride;
+    }
+}
+
+#ifdef RMD_DIAG
 // MFMA form (exact f32: v_mfma_f32_32x32x2_f32 == an fmaf chain): a workgroup owns 32 output
 // displacements x 128 pixels (4 waves x 32 pixels); its 32 rows of W (or of W^T) sit in LDS with an
 // odd row stride, x is read as two 128-B row segments per k-step.  grid (pixels/128, D/32, B).
@@ -1128,8 +1292,6 @@ dap_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int 
     }
 }
 
-
-#ifdef RMD_DIAG
 #ifndef RMD_DAP_KC
 #define RMD_DAP_KC 8
 #endif
@@ -1585,8 +1747,7 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
 #undef RMD_DAP
         return check_launch("rmd_dap/mfma");
     }
-#endif
-    if (disp <= 1024 && env_variant("RMD_DAP_VALU") == 0) {
+    if (disp <= 1024 && env_variant("RMD_DAP_VALU") == 1) {       // round-1 exact-f32 MFMA form
         const int Dk = (disp + 1) & ~1;
         const size_t lds = sizeof(float) * 32 * (size_t)(Dk + 1);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_kernel),
@@ -1594,6 +1755,61 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
         dim3 grid((pixels + 127) / 128, (disp + 31) / 32, batch);
         dap_mfma_kernel<<<grid, kThreads, lds, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
         return check_launch("rmd_dap/mfma");
+    }
+#endif
+    const int Kp = (disp + 15) & ~15;
+    if (disp <= 1024 && (long long)(Kp + 16) * pixels * 4 < (1ll << 31) && env_variant("RMD_DAP_VALU") == 0) {
+        // split-bf16 MFMA form: M-block of MT row tiles = the largest (<= 4) whose hi / lo W rows fit in
+        // 160 KB of LDS; 8 waves per workgroup when the block leaves room for only one workgroup per CU
+        const int mt_all = (disp + 31) / 32;
+        const size_t rowb = 2 * (size_t)(2 * Kp + 16);       // hi + lo bytes per W row
+        int mt = mt_all < 4 ? mt_all : 4;
+        while (mt > 1 && (size_t)32 * mt * rowb > 160 * 1024) --mt;
+        mt = std::min(mt, std::max(1, env_knob("RMD_DAP_MT", 4)));          // diagnostic: smaller M-blocks
+        const size_t lds = (size_t)32 * mt * rowb;
+        const int nw = env_knob("RMD_DAP_NW", 8) == 4 ? 4 : 8;      // diagnostic: 4-wave workgroups
+        const int mblocks = (mt_all + mt - 1) / mt;
+        const int ntile = (pixels + 31) / 32;
+        // one round of workgroups over the chip: ~256 x (workgroups per CU) in all, at least one
+        // 32-pixel tile per wave.  At 171-227 VGPRs a SIMD holds 2 waves, so a CU holds one 8-wave
+        // workgroup (measured against 4-wave workgroups, 2-3 per CU: 11.5 vs 13.2 us at D = 49, 13.1 vs
+        // 15.1 at D = 81, 62 vs 87 at D = 324 — fewer W stagings; profiles/dap_ab_r02.json)
+        const int occ = nw == 8 ? 1 : std::max(1, std::min(3, (int)((160 * 1024) / lds)));
+        const long long units = (long long)mblocks * batch;
+        int per = (int)std::min<long long>((256LL * occ + units - 1) / units, (ntile + nw - 1) / nw);
+        per = std::max(per, 1);
+        const long long nwg = units * per;
+        RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_dap: grid too large");
+        hipStream_t st = as_stream(stream);
+#define RMD_DAPX3(MT, NW)                                                                                   \
+        do {                                                                                                \
+            static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(dap_x3_kernel<MT, NW>), \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                                         160 * 1024) == hipSuccess;                        \
+            (void)attr;                                                                                     \
+            dap_x3_kernel<MT, NW><<<(unsigned)nwg, NW * 64, lds, st>>>(x, weight, disp, pixels, transpose,  \
+                                                                     mblocks, per, out);                    \
+        } while (0)
+        if (nw == 8) {
+            switch (mt) {
+                case 1: RMD_DAPX3(1, 8); break;
+                case 2: RMD_DAPX3(2, 8); break;
+                case 3: RMD_DAPX3(3, 8); break;
+                default: RMD_DAPX3(4, 8); break;
+            }
+        }
+#ifdef RMD_DIAG
+        else {
+            switch (mt) {
+                case 1: RMD_DAPX3(1, 4); break;
+                case 2: RMD_DAPX3(2, 4); break;
+                case 3: RMD_DAPX3(3, 4); break;
+                default: RMD_DAPX3(4, 4); break;
+            }
+        }
+#endif
+#undef RMD_DAPX3
+        return check_launch("rmd_dap/x3");
     }
     const size_t lds = sizeof(float) * (size_t)disp * disp;
     dim3 grid((pixels + kThreads - 1) / kThreads, batch);

@@ -2,7 +2,9 @@
 golden vectors (tests/golden) and the float64 oracle.
 
 Tolerances (max-normalised, conftest.rel_max_err): stacks 1e-5 (bilinear in pixel coordinates vs
-the reference's [-1,1] round trip), integer volume bit-exact (pure copy + mask), DAP 1e-5,
+the reference's [-1,1] round trip), integer volume bit-exact (pure copy + mask), DAP 1e-4 (north_star's
+fp32 tolerance; rmd_dap is a split-bf16 MFMA GEMM, hi.hi + hi.lo + lo.hi, measured ~1.5e-5 — the
+reference's own GPU conv runs in TF32 by default, ~5e-4), DAP weight gradient (torch GEMM) 1e-5,
 full modules through MatchingNet (MIOpen convolutions) 1e-4.
 """
 
@@ -12,6 +14,8 @@ import torch
 
 import oracle
 from conftest import load_golden, rel_max_err
+
+DAP_TOL = 1e-4
 from detinit import det_init
 
 pytestmark = pytest.mark.gpu
@@ -154,9 +158,9 @@ def test_dap_golden():
     x = _t(g["x"], True)
     wt = _t(g["weight"], True)
     y = rmd.ops.dap(x, wt)
-    assert rel_max_err(y.detach().cpu().numpy(), g["out"]) < 1e-5
+    assert rel_max_err(y.detach().cpu().numpy(), g["out"]) < DAP_TOL
     gx, gw = torch.autograd.grad(y, (x, wt), _t(g["grad_out"]))
-    assert rel_max_err(gx.cpu().numpy(), g["grad_x"]) < 1e-5
+    assert rel_max_err(gx.cpu().numpy(), g["grad_x"]) < DAP_TOL
     assert rel_max_err(gw.cpu().numpy(), g["grad_weight"]) < 1e-5
 
 
@@ -167,7 +171,25 @@ def test_dap_full_324_vs_oracle():
     x = rng.standard_normal((2, 324, 12, 16)).astype(np.float32)
     wt = (rng.standard_normal((324, 324, 1, 1)) * 0.05).astype(np.float32)
     y = rmd.ops.dap(_t(x), _t(wt)).cpu().numpy()
-    assert rel_max_err(y, oracle.dap(x.astype(np.float64), wt.astype(np.float64))) < 1e-5
+    assert rel_max_err(y, oracle.dap(x.astype(np.float64), wt.astype(np.float64))) < DAP_TOL
+
+
+@pytest.mark.parametrize("transpose", [False, True])
+@pytest.mark.parametrize("b,d,h,w", [(3, 25, 7, 9), (2, 130, 5, 13), (1, 200, 33, 1), (2, 1, 4, 4),
+                                     (1, 1000, 3, 5), (2, 324, 12, 16)])
+def test_dap_ragged_vs_oracle(b, d, h, w, transpose):
+    """rmd_dap's split-bf16 MFMA GEMM at ragged shapes: D not a multiple of 16 or 32, several M-blocks
+    (D = 130, 200: 2 blocks; 324: 4; 1000: 32 one-tile blocks, 8-wave workgroups), pixel counts that are
+    not a multiple of the 32-pixel tile, D = 1; forward and transposed (the input gradient W^T g)."""
+    import rmd  # noqa: F401
+    rng = np.random.default_rng(d * 7 + h)
+    x = rng.standard_normal((b, d, h, w)).astype(np.float32)
+    wt = (np.eye(d) + rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)
+    op = torch.ops.rmd.dap_transpose if transpose else torch.ops.rmd.dap
+    y = op(_t(x), _t(wt[:, :, None, None])).cpu().numpy()
+    w64 = wt.astype(np.float64)
+    ref = oracle.dap(x.astype(np.float64), (w64.T if transpose else w64)[:, :, None, None])
+    assert rel_max_err(y, ref) < DAP_TOL
 
 
 @pytest.mark.parametrize("dap_type", ["separate", "full"])

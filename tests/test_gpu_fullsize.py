@@ -9,7 +9,8 @@ Tolerances are ELEMENTWISE (conftest.assert_close_elementwise: |got - ref| <= at
   * integer DICL volume (cfg3, copy + mask): bit-exact
   * bilinear DICL stack (cfg4 levels): rtol 1e-5, atol 1e-6 — fp32 pixel-coordinate bilinear vs the
     float64 restatement
-  * DAP (cfg3 D=49, cfg4 D=81): rtol 1e-5, atol 1e-5 * max|ref| — K-long fp32 dot products
+  * DAP (cfg3 D=49, cfg4 D=81): rtol 5e-5, atol 5e-5 * max|ref| — split-bf16 MFMA (hi.hi + hi.lo +
+    lo.hi, fp32 accumulate): ~1.5e-5 * max|ref| absolute
 SURVEY.md §8(d): cfg3 = DICL 384x512 b8, levels 2..6 (96x128 .. 6x8), C=32, D=49; cfg4 = KITTI
 376x1242 padded to 384x1280, ctf-l3 levels 1/8, 1/16, 1/32 (48x160, 24x80, 12x40), C=32, D=81.
 """
@@ -91,7 +92,7 @@ def test_cfg4_dicl_stack_b8(level, h, w):
     assert bool((st[:, :, :, :c] == f1t).all())                       # no mask on the bilinear stack
 
 
-@pytest.mark.parametrize("d,h,w", [(49, 96, 128), (81, 48, 160)])
+@pytest.mark.parametrize("d,h,w", [(49, 96, 128), (81, 48, 160), (324, 48, 160)])
 def test_dap_b8_full_size(d, h, w):
     import rmd
     rng = np.random.default_rng(d)
@@ -104,4 +105,4 @@ def test_dap_b8_full_size(d, h, w):
     bi, yi, xi = _sample(rng, (b, h, w), n)
     got = y[torch.from_numpy(bi).to(DEV), :, torch.from_numpy(yi).to(DEV), torch.from_numpy(xi).to(DEV)]
     ref = x.astype(np.float64)[bi, :, yi, xi] @ wt[:, :, 0, 0].astype(np.float64).T    # (n, D)
-    assert_close_elementwise(got.cpu().numpy(), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    assert_close_elementwise(got.cpu().numpy(), ref, rtol=5e-5, atol=5e-5 * np.abs(ref).max())

@@ -3,7 +3,8 @@ against reference golden vectors (tests/golden/heads_*.npz, made by tests/golden
 and the float64 oracle (oracle/heads.py).
 
 Tolerances (max-normalised, conftest.rel_max_err): kernels vs oracle 1e-5 (fp32 softmax/expf vs
-float64); whole modules with MIOpen convolutions vs the reference's fp32 CPU autograd 1e-4.
+float64); whole modules with MIOpen convolutions vs the reference's fp32 CPU autograd 1e-4; modules
+with a DAP layer 1e-4 (north_star's fp32 tolerance: rmd_dap computes in split-bf16 MFMA, ~1.5e-5).
 Edge cases: 1-pixel and 1-row maps (every neighbour tap out of bounds), large logits (softmax
 overflow safety), non-multiple-of-wave pixel counts, extra trailing channels (dicl_emb).
 """
@@ -94,12 +95,13 @@ def test_softargmax_raft_matches_reference_golden(kind):
     mod = _dap_sd(mod)
     cost = _t(g["cost"], True)
     flows = mod(cost)
+    tol = 1e-4 if kind == "dap" else 1e-5
     assert len(flows) == L
     for i, f in enumerate(flows):
-        assert rel_max_err(f.detach().cpu().numpy(), g[f"flow{i}"]) < 1e-5
+        assert rel_max_err(f.detach().cpu().numpy(), g[f"flow{i}"]) < tol
     loss = sum((f * _t(g[f"grad_flow{i}"])).sum() for i, f in enumerate(flows))
     (dc,) = torch.autograd.grad(loss, cost)
-    assert rel_max_err(dc.cpu().numpy(), g["grad_cost"]) < 1e-5
+    assert rel_max_err(dc.cpu().numpy(), g["grad_cost"]) < tol
 
 
 @pytest.mark.parametrize("cmod", ["dot", "dicl", "dicl-1x1", "dicl-emb"])
@@ -117,10 +119,11 @@ def test_softargmax_corr_module_matches_reference_golden(cmod, kind):
         cost_np = np.concatenate([cost_np, extra], axis=1)
     cost = _t(cost_np, True)
     f = mod(cost)
-    assert rel_max_err(f.detach().cpu().numpy(), g["flow"]) < 1e-5
+    tol = 1e-4 if kind == "dap" else 1e-5
+    assert rel_max_err(f.detach().cpu().numpy(), g["flow"]) < tol
     (dc,) = torch.autograd.grad(f, cost, _t(g["grad_flow"]))
     dd = (2 * r + 1) ** 2
-    assert rel_max_err(dc[:, :dd].cpu().numpy(), g["grad_cost"]) < 1e-5
+    assert rel_max_err(dc[:, :dd].cpu().numpy(), g["grad_cost"]) < tol
     assert not dc[:, dd:].any()
 
 

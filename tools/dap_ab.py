@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the DAP kernels (diagnostic build: RMD_LIBRARY=raft-meets-dicl_amd/rmd/librmd_diag.so).
-Variants (RMD_AB, comma-separated, '+'-joined NAME=VALUE env settings): e.g. "RMD_DAP_VALU=2"
-(round-1 MFMA kernel), "RMD_DAP_TPW=1", "RMD_DAP_TPW=2".  Shapes: D=49 at cfg3 level 2 (96x128),
+Variants (RMD_AB, comma-separated, '+'-joined NAME=VALUE env settings): "RMD_DAP_VALU=0" (product:
+split-bf16 x3 MFMA), "RMD_DAP_VALU=1" (round-1 exact-f32 MFMA), "RMD_DAP_VALU=2" (VALU),
+"RMD_DAP_VALU=3" (blocked exact-f32 MFMA, RMD_DAP_TPW tiles per wave).  Shapes: D=49 at cfg3 level 2 (96x128),
 D=81 at cfg4 1/8 (48x160), D=324 'full' (48x160), batch 8; forward and transposed (input gradient).
 Outputs compared with the first variant; median of `reps` HIP-event timings.
 usage: python tools/dap_ab.py [reps] -> JSON"""
@@ -17,13 +18,13 @@ import torch  # noqa: E402
 def main():
     from rmd import ops
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    names = os.environ.get("RMD_AB", "RMD_DAP_VALU=2,RMD_DAP_TPW=1,RMD_DAP_TPW=2").split(",")
+    names = os.environ.get("RMD_AB", "RMD_DAP_VALU=0,RMD_DAP_VALU=1").split(",")
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     res = {}
 
     def select(n):
-        for k in ("RMD_DAP_VALU", "RMD_DAP_TPW", "RMD_DAP_STREAM"):
+        for k in ("RMD_DAP_VALU", "RMD_DAP_TPW", "RMD_DAP_STREAM", "RMD_DAP_MT", "RMD_DAP_NW"):
             os.environ.pop(k, None)
         for kv in filter(None, n.split("+")):
             k, v = kv.split("=")
@@ -36,6 +37,8 @@ def main():
         for tr in (False, True):
             key = f"D{d}_{h}x{w}_b8" + ("_transpose" if tr else "")
             fn = (lambda: torch.ops.rmd.dap_transpose(x, wt)) if tr else (lambda: ops.dap(x, wt))
+            w64 = wt[:, :, 0, 0].double()
+            ref = torch.einsum("oi,bihw->bohw", w64.t() if tr else w64, x.double())
             outs, times = {}, {}
             for n in names:
                 select(n)
@@ -53,7 +56,10 @@ def main():
                 ts.sort()
                 times[n] = ts[len(ts) // 2] * 1e3
             res[key] = {n: {"median_us": times[n], "GBps": nbytes / (times[n] * 1e-6) / 1e9,
-                            "max_abs_diff_first": float((outs[n] - outs[names[0]]).abs().max())} for n in names}
+                            "max_abs_diff_first": float((outs[n] - outs[names[0]]).abs().max()),
+                            "max_norm_err_fp64": float((outs[n].double() - ref).abs().max() / ref.abs().max()),
+                            "max_elem_rel_err_fp64": float(((outs[n].double() - ref).abs()
+                                                            / (ref.abs() + 1e-3 * ref.abs().max())).max())} for n in names}
     print(json.dumps(res, indent=1))
 
 
