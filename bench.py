@@ -67,6 +67,11 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=6, help="frame pairs per GPU (train/chairs2-1 stage)")
+    ap.add_argument("--hybrid", choices=["on", "off"], default="on",
+                    help="extra leg: RAFT+DICL ctf-l3 inference at 376x1242 (BASELINE configs[3]) on every rank")
+    ap.add_argument("--hybrid-steps", type=int, default=5)
+    ap.add_argument("--hybrid-warmup", type=int, default=2)
+    ap.add_argument("--hybrid-batch", type=int, default=8, help="frame pairs per GPU (weak; --global-batch splits)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (pair with --backend gloo)")
@@ -270,6 +275,63 @@ def train_leg(args, world, rank, device):
             "scaling": "weak", "dtype": "fp32", "data": "synthetic smooth pairs with known flow, name-keyed random weights"}
 
 
+def hybrid_leg(args, world, rank, device):
+    """BASELINE configs[3] / SURVEY.md §8(d) cfg4: RAFT+DICL ctf-l3 inference on KITTI-shape pairs
+    (376x1242 padded to 384x1280, ModuloPadding 64), iterations (4, 3, 3), convex upsampling, batch
+    sharded over the ranks with no collective on the data path (per-GPU b8 weak scaling, or
+    --global-batch G split evenly: strong).  The correlation modules are rmd.corr.make_cmod('dicl')
+    (the HIP DICL stack + MatchingNet on MIOpen + the split-bf16 DAP), the GRU update blocks stay
+    PyTorch, the convex upsampling is rmd Up8 — the reference's raft_dicl_ctf_l3.py:79-260 through
+    tests/e2e/ctf_l3_net.py.  The timed region (MAX over ranks) is whole forward passes."""
+    for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import rmd
+    from detinit import det_init_fanin
+    from e2e.ctf_l3_net import CtfL3Net
+    from synth import frame_pair
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    h, w, pad = 376, 1242, 64
+    bsz = args.global_batch // world if args.global_batch else args.hybrid_batch
+    net = det_init_fanin(CtfL3Net(rmd.corr.make_cmod, rmd.corr.make_flow_regression, upnet_cls=rmd.raft.Up8Network),
+                         head_gain=0.02).to(device).eval()
+    i1s, i2s = [], []
+    for k in range(bsz):
+        seed = 5000 + 1000 * rank + k
+        rng = np.random.default_rng(seed)
+        i1, i2, _ = frame_pair(h, w, flow=tuple(int(v) for v in rng.integers(0, 8, 2)), seed=seed, pad=pad)
+        i1s.append(i1), i2s.append(i2)
+    img1, img2 = (torch.from_numpy(np.concatenate(x)).to(device) for x in (i1s, i2s))
+    with torch.no_grad():
+        for _ in range(args.hybrid_warmup):
+            net(img1, img2, (4, 3, 3))
+        torch.cuda.synchronize(device)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(args.hybrid_steps):
+            out = net(img1, img2, (4, 3, 3))
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    el = job_time(el, world, device)
+    fin = bool(torch.isfinite(out[-1][-1]).all())
+    hp, wp = img1.shape[-2:]
+    del net, out, img1, img2
+    torch.cuda.empty_cache()
+    return {"workload": "RAFT+DICL ctf-l3 inference (BASELINE configs[3], SURVEY cfg4): 376x1242 padded "
+                        f"{hp}x{wp}, iterations (4,3,3), convex upsampling",
+            "frame_pairs_per_s": world * bsz * args.hybrid_steps / el, "ms_per_batch": el / args.hybrid_steps * 1e3,
+            "per_gpu_batch": bsz, "global_batch": world * bsz, "n_gpus": world, "steps": args.hybrid_steps,
+            "warmup": args.hybrid_warmup, "parallelism": f"batch-shard x{world} (no collective)",
+            "scaling": "strong" if args.global_batch else "weak", "dtype": "fp32", "finite": fin,
+            "convs": "MIOpen fp32 (TF32 off)",
+            "data": "synthetic smooth pairs (tests/golden/synth.py), name-keyed random weights"}
+
+
 def job_time(elapsed, world, device):
     """Whole-job time of the timed region: the MAX over ranks (one all_reduce after the region,
     nothing on the data path); identity for a single process."""
@@ -442,6 +504,10 @@ def main():
         res["roofline_lookup"] = roof_look
         if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
             res["model_level"] = model_level(device, args.precision)
+        if args.hybrid == "on":
+            hy = hybrid_leg(args, world, rank, device)     # every rank (batch shards, job-time MAX)
+            if rank == 0:
+                res["hybrid_inference"] = hy
         if args.train == "on":
             tr = train_leg(args, world, rank, device)      # every rank (DDP collectives)
             if rank == 0:
