@@ -368,10 +368,12 @@ def init_distributed(args):
         torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
+        import datetime
+        tmo = datetime.timedelta(seconds=600)          # a stuck collective raises instead of hanging forever
         if device.type == "cuda" and args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=tmo)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=tmo)
         assert dist.get_world_size() == world
     return world, rank, device
 
@@ -504,14 +506,19 @@ def main():
         res["roofline_lookup"] = roof_look
         if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
             res["model_level"] = model_level(device, args.precision)
-        if args.hybrid == "on":
-            hy = hybrid_leg(args, world, rank, device)     # every rank (batch shards, job-time MAX)
+        # extra legs run on every rank (batch shards / DDP collectives); a Python-level failure in one
+        # (raised symmetrically on every rank, e.g. out of memory) is recorded instead of losing the
+        # headline line
+        for flag, key, leg in ((args.hybrid, "hybrid_inference", hybrid_leg), (args.train, "train_step", train_leg)):
+            if flag != "on":
+                continue
+            try:
+                out = leg(args, world, rank, device)
+            except Exception as e:                      # noqa: BLE001 — reported in the JSON line
+                out = {"error": f"{type(e).__name__}: {e}"[:500]}
+                torch.cuda.empty_cache()
             if rank == 0:
-                res["hybrid_inference"] = hy
-        if args.train == "on":
-            tr = train_leg(args, world, rank, device)      # every rank (DDP collectives)
-            if rank == 0:
-                res["train_step"] = tr
+                res[key] = out
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args)
