@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--hybrid-steps", type=int, default=5)
     ap.add_argument("--hybrid-warmup", type=int, default=2)
     ap.add_argument("--hybrid-batch", type=int, default=8, help="frame pairs per GPU (weak; --global-batch splits)")
+    ap.add_argument("--dicl", choices=["on", "off"], default="on",
+                    help="extra leg: DICL cost volumes + MatchingNet coarse-to-fine at 384x512 (BASELINE configs[2])")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (pair with --backend gloo)")
@@ -332,6 +334,81 @@ def hybrid_leg(args, world, rank, device):
             "data": "synthetic smooth pairs (tests/golden/synth.py), name-keyed random weights"}
 
 
+def dicl_leg(args, world, rank, device):
+    """BASELINE configs[2] / SURVEY.md §8(d) cfg3: the DICL baseline's matching stage coarse to fine at
+    384x512, per-GPU b8, C = 32, displacement range (3, 3) (D = 49) on levels 6..2 (6x8 .. 96x128):
+    per level the coarse flow upsampled x2 (impls/dicl.py:171-181), the warped masked integer volume
+    (rmd_dicl_stack_int_warped: warp + a8 in one kernel pair, impls/dicl.py:178-238), MatchingNet
+    (MIOpen, blocks/dicl.py:93-118), DAP (rmd_dap, split-bf16 MFMA) and the soft-argmin flow
+    regression (impls/dicl.py:53-86, torch).  Feature maps are synthetic (the feature encoder and
+    the context networks are outside §8); weights: torch default init, DAP identity, BN in eval."""
+    import torch.nn.functional as F
+    from rmd import ops
+    from rmd.blocks.dicl import DisplacementAwareProjection, MatchingNet
+    torch.backends.cudnn.allow_tf32 = False
+    b = args.global_batch // world if args.global_batch else 8
+    c, md, levels = 32, (3, 3), (6, 5, 4, 3, 2)
+    g = torch.Generator().manual_seed(77 + rank)
+    torch.manual_seed(77)
+    mods = {}
+    feats = {}
+    for l in levels:
+        h, w = 384 >> l, 512 >> l
+        mods[l] = (MatchingNet(2 * c).to(device).eval(), DisplacementAwareProjection(md).to(device).eval())
+        feats[l] = tuple(torch.randn(b, c, h, w, generator=g).to(device) for _ in range(2))
+    du, dv = 2 * md[0] + 1, 2 * md[1] + 1
+    disp = torch.stack(torch.meshgrid(torch.arange(-md[0], md[0] + 1.0), torch.arange(-md[1], md[1] + 1.0),
+                                      indexing="ij")).view(1, 2, du, dv, 1, 1).to(device)
+    vol_bytes = 0
+
+    def forward():
+        nonlocal vol_bytes
+        flow, vb = None, 0
+        for l in levels:
+            f1, f2 = feats[l]
+            h, w = f1.shape[-2:]
+            mnet, dap = mods[l]
+            if flow is None:
+                mvol = ops.dicl_stack_int(f1, f2, md[0], md[1])
+            else:
+                up = 2.0 * F.interpolate(flow, (h, w), mode="bilinear", align_corners=True)
+                mvol = ops.dicl_stack_int_warped(f1, f2, up, md[0], md[1])
+            vb += mvol.numel() * 4
+            cost = dap(mnet(mvol))
+            prob = F.softmax(cost.reshape(b, du * dv, h, w), dim=1).view(b, 1, du, dv, h, w)
+            lf = (prob * disp).sum(dim=(2, 3))
+            flow = lf if flow is None else lf + up
+        vol_bytes = vb
+        return flow
+
+    with torch.no_grad():
+        for _ in range(3):
+            forward()
+        torch.cuda.synchronize(device)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(device)
+        reps = 10
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = forward()
+        torch.cuda.synchronize(device)
+        el = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier()
+    el = job_time(el, world, device)
+    fin = bool(torch.isfinite(out).all())
+    del mods, feats, out
+    torch.cuda.empty_cache()
+    return {"workload": "DICL cost volumes + MatchingNet + DAP + soft-argmin, coarse to fine (levels 6..2) at "
+                        "384x512 (BASELINE configs[2], SURVEY cfg3)",
+            "frame_pairs_per_s": world * b * reps / el, "ms_per_batch": el / reps * 1e3, "per_gpu_batch": b,
+            "global_batch": world * b, "n_gpus": world, "volume_bytes_per_batch": vol_bytes,
+            "displacement_range": list(md), "channels": c, "finite": fin,
+            "scaling": "strong" if args.global_batch else "weak", "dtype": "fp32",
+            "data": "synthetic feature maps (encoder / context nets outside the hot path)"}
+
+
 def job_time(elapsed, world, device):
     """Whole-job time of the timed region: the MAX over ranks (one all_reduce after the region,
     nothing on the data path); identity for a single process."""
@@ -509,7 +586,8 @@ def main():
         # extra legs run on every rank (batch shards / DDP collectives); a Python-level failure in one
         # (raised symmetrically on every rank, e.g. out of memory) is recorded instead of losing the
         # headline line
-        for flag, key, leg in ((args.hybrid, "hybrid_inference", hybrid_leg), (args.train, "train_step", train_leg)):
+        for flag, key, leg in ((args.dicl, "dicl_matching", dicl_leg), (args.hybrid, "hybrid_inference", hybrid_leg),
+                               (args.train, "train_step", train_leg)):
             if flag != "on":
                 continue
             try:
