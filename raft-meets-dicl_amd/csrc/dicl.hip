@@ -1096,12 +1096,14 @@ typedef __attribute__((ext_vector_type(4))) __bf16 dbf16x4_t;
 // (or the next tile's first) in flight during the current chunk's MFMAs.  Rows >= D and pixels >= n
 // fall outside the per-image buffer range (loads read 0, stores are dropped).  The M-blocks of one
 // pixel chunk are consecutive workgroup ids (one XCD), so x is fetched from HBM once for all blocks.
-// Measured (profiles/dap_ab_r02.json, b8): D = 49 11.5 us, D = 81 13.1 us, D = 324 62 us, vs 16.8 /
-// 23.2 / 317 us for the exact-f32 MFMA form; error vs float64 1.5e-5 max-normalised.  At D = 324 the
-// MFMA floor is ~19 us and the HBM floor ~27 us: the two waves per SIMD wait on each chunk's x loads
-// (one chunk of prefetch distance in registers); staging x through LDS asynchronously is the next step.
-constexpr int kDapKC = 8;     // k-steps per x chunk (double-buffered)
+// Output stores are non-temporal.  Measured (profiles/dap_ab_r02.json, b8): D = 49 10.1 us, D = 81
+// 12.1 us, D = 324 62 us, vs 16.8 / 23.2 / 317 us for the exact-f32 MFMA form; error vs float64
+// 1.5e-5 max-normalised.  At D = 324 the MFMA floor is ~19 us and the HBM floor ~27 us; PMC shows x
+// fetched from HBM once (84 MB) and the x ring depth (3-8 chunks of prefetch) changes nothing, so the
+// gap is in the per-CU issue of the 4x L2 re-reads of x and the single 8-wave workgroup per CU.
 constexpr int kDapSG = 4;     // W staging: 4-element groups per thread in flight
+constexpr int kDapStoreAux = 2;   // output store cache policy (gfx950 cpol: 2 = nt): 10-15 % at D <= 81
+constexpr int kDapKC = 8, kDapNB = 2;   // x ring: NB buffers of KC k-steps
 
 __device__ __forceinline__ void dap_split8(const float* v, dbf16x8_t& hi, dbf16x8_t& lo) {
 #pragma unroll
@@ -1111,7 +1113,7 @@ __device__ __forceinline__ void dap_split8(const float* v, dbf16x8_t& hi, dbf16x
     }
 }
 
-template <int MT, int NW>
+template <int MT, int NW, int AUX, int KC, int NB>
 __global__ void __launch_bounds__(NW * 64, 2)
 dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
               int mblocks, int per, float* __restrict__ out) {
@@ -1140,25 +1142,30 @@ dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D,
     const __amdgpu_buffer_rsrc_t orr = rsrc(out + (size_t)b * D * n);
     const unsigned rowb = (unsigned)n * 4u;
     const unsigned aoff = (unsigned)(r * RB + 16 * h);
-    const int nch = (nks + kDapKC - 1) / kDapKC;
+    const int nch = (nks + KC - 1) / KC;
 
-    float xc[kDapKC * 8], xn[kDapKC * 8];
+    // x chunks stream through a ring of NB register buffers: step i = (tile t0 + (i / nch) tstride,
+    // chunk i % nch) lives in buffer i % NB and is loaded NB - 1 steps before its use
+    float xb[NB][KC * 8];
     // chunk c of tile tt: rows 16 (KC c + u) + 8 h + j at pixel 32 tt + r (out of range past n / D)
-    auto load = [&](float (&v)[kDapKC * 8], int tt, int c) {
+    auto load = [&](float (&v)[KC * 8], int tt, int c) {
         const int p = tt * 32 + r;
-        const unsigned base = p < n ? (unsigned)(8 * h + 16 * kDapKC * c) * rowb + (unsigned)p * 4u : 0x80000000u;
+        const unsigned base = p < n ? (unsigned)(8 * h + 16 * KC * c) * rowb + (unsigned)p * 4u : 0x80000000u;
 #pragma unroll
-        for (int u = 0; u < kDapKC; ++u)
-            if (kDapKC * c + u < nks)
+        for (int u = 0; u < KC; ++u)
+            if (KC * c + u < nks)
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     v[u * 8 + j] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                         xr, (int)(base + (unsigned)(16 * u + j) * rowb), 0, 0));
     };
 
-    int t = pc * NW + w;
-    const int tstride = per * NW;
-    if (t < ntile) load(xc, t, 0);          // in flight while the workgroup stages W
+    const int t0 = pc * NW + w, tstride = per * NW;
+    const int mytiles = t0 < ntile ? (ntile - 1 - t0) / tstride + 1 : 0;
+    const int nsteps = mytiles * nch;
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)        // in flight while the workgroup stages W
+        if (u < nsteps) load(xb[u], t0 + (u / nch) * tstride, u % nch);
 
     // stage the block's W rows as hi / lo bf16 (4 consecutive k per thread; W^T reads run along o),
     // kDapSG groups' loads in flight per thread before any is converted
@@ -1199,20 +1206,25 @@ dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D,
     }
     __syncthreads();
 
-    while (t < ntile) {
-        f32x16_t acc[MT];
+    f32x16_t acc[MT];
+    for (int i0 = 0; i0 < nsteps; i0 += NB) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] = f32x16_t{};
-        for (int c = 0; c < nch; ++c) {
-            int tn = t, cn = c + 1;
-            if (cn == nch) { tn = t + tstride; cn = 0; }
-            if (tn < ntile) load(xn, tn, cn);
+        for (int u = 0; u < NB; ++u) {
+            const int i = i0 + u;
+            if (i >= nsteps) break;
+            const int ip = i + NB - 1;
+            if (ip < nsteps) load(xb[(u + NB - 1) % NB], t0 + (ip / nch) * tstride, ip % nch);
+            const int c = i % nch;
+            if (c == 0) {
 #pragma unroll
-            for (int u = 0; u < kDapKC; ++u) {
-                const int s = c * kDapKC + u;
+                for (int m = 0; m < MT; ++m) acc[m] = f32x16_t{};
+            }
+#pragma unroll
+            for (int uu = 0; uu < KC; ++uu) {
+                const int s = c * KC + uu;
                 if (s < nks) {
                     dbf16x8_t bh, bl;
-                    dap_split8(xc + u * 8, bh, bl);
+                    dap_split8(xb[u] + uu * 8, bh, bl);
 #pragma unroll
                     for (int m = 0; m < MT; ++m) {
                         const unsigned a = aoff + (unsigned)(m * 32 * RB + 32 * s);
@@ -1225,20 +1237,20 @@ dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D,
                     }
                 }
             }
+            if (c == nch - 1) {
+                // C tile: lane (r, h) holds rows 8 (e >> 2) + 4 h + (e & 3) of pixel column r
+                const int p = (t0 + (i / nch) * tstride) * 32 + r;
+                const unsigned so = p < n ? (unsigned)(4 * h) * rowb + (unsigned)p * 4u : 0x80000000u;
 #pragma unroll
-            for (int q = 0; q < kDapKC * 8; ++q) xc[q] = xn[q];
-        }
-        // C tile: lane (r, h) holds rows 8 (e >> 2) + 4 h + (e & 3) of pixel column r
-        const int p = t * 32 + r;
-        const unsigned so = p < n ? (unsigned)(4 * h) * rowb + (unsigned)p * 4u : 0x80000000u;
+                for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const unsigned row = (unsigned)(o0 + m * 32 + 8 * (e >> 2) + (e & 3));
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[m][e]), orr, (int)(so + row * rowb), 0, 0);
+                    for (int e = 0; e < 16; ++e) {
+                        const unsigned row = (unsigned)(o0 + m * 32 + 8 * (e >> 2) + (e & 3));
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[m][e]), orr, (int)(so + row * rowb),
+                                                              0, AUX);
+                    }
             }
-        t += tstride;
+        }
     }
 }
 
@@ -1781,15 +1793,34 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
         const long long nwg = units * per;
         RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_dap: grid too large");
         hipStream_t st = as_stream(stream);
+#define RMD_DAPX3_R(MT, NW, AUX, KC, NB)                                                                    \
+        do {                                                                                                \
+            static const bool attr = hipFuncSetAttribute(                                                   \
+                reinterpret_cast<const void*>(dap_x3_kernel<MT, NW, AUX, KC, NB>),                          \
+                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;                      \
+            (void)attr;                                                                                     \
+            dap_x3_kernel<MT, NW, AUX, KC, NB><<<(unsigned)nwg, NW * 64, lds, st>>>(x, weight, disp, pixels, \
+                                                                                  transpose, mblocks, per, out); \
+        } while (0)
+#ifdef RMD_DIAG
+        const int dap_nt = env_knob("RMD_DAP_NT", kDapStoreAux);              // diagnostic: store policy
+        const int dap_ring = env_knob("RMD_DAP_RING", 0);                     // diagnostic: x ring shape
+#define RMD_DAPX3_A(MT, NW, AUX)                                                                            \
+        do {                                                                                                \
+            switch (dap_ring) {                                                                             \
+                case 1: RMD_DAPX3_R(MT, NW, AUX, 4, 3); break;                                              \
+                case 2: RMD_DAPX3_R(MT, NW, AUX, 4, 4); break;                                              \
+                case 3: RMD_DAPX3_R(MT, NW, AUX, 2, 8); break;                                              \
+                default: RMD_DAPX3_R(MT, NW, AUX, kDapKC, kDapNB); break;                                  \
+            }                                                                                               \
+        } while (0)
 #define RMD_DAPX3(MT, NW)                                                                                   \
         do {                                                                                                \
-            static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(dap_x3_kernel<MT, NW>), \
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize,       \
-                                                         160 * 1024) == hipSuccess;                        \
-            (void)attr;                                                                                     \
-            dap_x3_kernel<MT, NW><<<(unsigned)nwg, NW * 64, lds, st>>>(x, weight, disp, pixels, transpose,  \
-                                                                     mblocks, per, out);                    \
+            if (dap_nt == 2) RMD_DAPX3_A(MT, NW, 2); else RMD_DAPX3_A(MT, NW, 0);                           \
         } while (0)
+#else
+#define RMD_DAPX3(MT, NW) RMD_DAPX3_R(MT, NW, kDapStoreAux, kDapKC, kDapNB)
+#endif
         if (nw == 8) {
             switch (mt) {
                 case 1: RMD_DAPX3(1, 8); break;
@@ -1809,6 +1840,8 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
         }
 #endif
 #undef RMD_DAPX3
+#undef RMD_DAPX3_A
+#undef RMD_DAPX3_R
         return check_launch("rmd_dap/x3");
     }
     const size_t lds = sizeof(float) * (size_t)disp * disp;

@@ -10,3 +10,11 @@ timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$
 python3 tools/trace_summary.py $(find gpurun_out/${TAG}_tr -name "*kernel_trace.csv" | head -1) dap > gpurun_out/${TAG}_trace.txt
 find gpurun_out/${TAG}_tr -name "*kernel_trace.csv" -delete
 echo done
+if [ -n "$PMC" ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/${TAG}_pmc_$c -o run -- python3 tools/dap_ab.py 2 > gpurun_out/${TAG}_pmc_$c.log 2>&1 || exit 5
+    python3 tools/pmc_kernel_avg.py $(find gpurun_out/${TAG}_pmc_$c -name "*counter_collection.csv" | head -1) dap > gpurun_out/${TAG}_pmc_$c.txt
+    find gpurun_out/${TAG}_pmc_$c -name "*counter_collection.csv" -delete
+  done
+fi
+echo pmc-done

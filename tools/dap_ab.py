@@ -24,7 +24,7 @@ def main():
     res = {}
 
     def select(n):
-        for k in ("RMD_DAP_VALU", "RMD_DAP_TPW", "RMD_DAP_STREAM", "RMD_DAP_MT", "RMD_DAP_NW"):
+        for k in ("RMD_DAP_VALU", "RMD_DAP_TPW", "RMD_DAP_STREAM", "RMD_DAP_MT", "RMD_DAP_NW", "RMD_DAP_NT", "RMD_DAP_RING"):
             os.environ.pop(k, None)
         for kv in filter(None, n.split("+")):
             k, v = kv.split("=")
