@@ -136,16 +136,21 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * Backward of the RAFT correlation (training; autograd of raft.py:18-95).  Coordinates are
  * detached in the reference (raft.py:402), so only the feature maps receive gradients.
  *
- * Gradient of the pyramid, dense float32 "G": (B, T, N) row-major, query-minor (the forward
- * pyramid's orientation), T = rmd_corr_grad_targets() = sum_l H_l*W_l; level l occupies rows
- * [t_off(l), t_off(l) + H_l*W_l) with t_off(l) = sum_{l'<l} H_l'*W_l' and target (y, x) at row
- * t_off(l) + y*W_l + x, query p in column p.  With P = rmd_corr_pool_targets(fmap2, scale =
- * 1/sqrt(C)) as (B, C, T):
- *   grad_fmap1 (B, C, N) = P G    and    dP (B, C, T) = fmap1 G^T      (rmd_corr_grad_gemm)
+ * Gradient of the pyramid, dense float32 "G", in the forward pyramid's chunked query-minor order
+ * with 8-target chunks: target row (l, y) is cut into nch(l) = ceil(W_l/8) chunks, chunk
+ * ch(l, y, x) = coff(l) + y*nch(l) + x/8 with coff(l) = sum_{l'<l} H_l'*nch(l'), TC chunks per image,
+ * and element (b, target (l, y, x), query p) at ((b*TC + ch)*N + p)*8 + x%8.  Seen as a matrix over
+ * the padded targets t' = 8*ch + x%8 (T' = 8*TC = rmd_corr_grad_targets(); pad targets x >= W_l stay
+ * zero) G is (T' x N) stored in 8-row blocks.  With P = rmd_corr_pool_targets(fmap2, scale =
+ * 1/sqrt(C)) as (B, C, T') in the same target order:
+ *   grad_fmap1 (B, C, N) = P G     (rmd_corr_grad_gemm layout 3, lda = T', ldb = N)
+ *   dP (B, C, T') = fmap1 G^T      (rmd_corr_grad_gemm layout 2, lda = N, ldb = N)
  *   grad_fmap2 = rmd_corr_unpool_targets(dP, scale = 1/sqrt(C)).
+ * A wave of 64 consecutive queries whose (smooth) flow moves their windows one column per query
+ * touches 3 128-B lines per 8 lanes at every tap (8 lines in a plain (B, T, N) order).
  */
 
-/* Targets per query row of G (all levels), or -1 on bad sizes.  Host-only. */
+/* Padded targets per image of G (T' = 8 * chunks over all levels), or -1 on bad sizes.  Host-only. */
 long long rmd_corr_grad_targets(int height, int width, int levels);
 
 /* grad_levels (G, caller-zeroed once per forward) += d(lookup)/d(pyramid)^T grad_out, where
@@ -155,21 +160,25 @@ long long rmd_corr_grad_targets(int height, int width, int levels);
 int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* desc, const float* coords,
                              int radius, unsigned zero_level_mask, float* grad_levels, void* stream);
 
-/* pooled (B, C, T) = avg_pool_{2^l}(fmap2) * scale for every level (raft.py:35-47 applied to the
- * feature map, which commutes with the product). */
+/* pooled (B, C, T') = avg_pool_{2^l}(fmap2) * scale for every level, in G's padded target order (pad
+ * targets 0) (raft.py:35-47 applied to the feature map, which commutes with the product). */
 int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,
                           float scale, float* pooled, void* stream);
 
-/* grad_fmap2 (B, C, H, W) = scale * sum_l avg_pool_{2^l}^T(grad_pooled level l)  (avg_pool2d_backward). */
+/* grad_fmap2 (B, C, H, W) = scale * sum_l avg_pool_{2^l}^T(grad_pooled level l)  (avg_pool2d_backward);
+ * grad_pooled is (B, C, T') in G's padded target order. */
 int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
                             float scale, float* grad_fmap2, void* stream);
 
 /* The two GEMMs of the backward (autograd of the matmul at raft.py:31-33), fp32-accurate from three
  * split-bf16 MFMA products (hi.hi + hi.lo + lo.hi), batched over `batch`:
  *   out[b] (m x nc, row-major) = a[b] (m x k, row stride lda) . B[b]
- *   layout 0: B = bm[b] given as k x nc (row stride ldb >= nc)       -> grad_fmap1 = P G
- *   layout 1: B = bm[b]^T, bm[b] given as nc x k (row stride ldb >= k) -> dP = fmap1 G^T
- * Batch strides are m*lda for a and (layout 0 ? k : nc)*ldb for bm; out is contiguous.  K may be
+ *   layout 0: B element (k, n) at bm[k*ldb + n]                 (k x nc, ldb >= nc)
+ *   layout 1: B element (k, n) at bm[n*ldb + k]                 (nc x k, ldb >= k)
+ *   layout 2: B element (k, n) at bm[((n/8)*ldb + k)*8 + n%8]   (ldb >= k)  -> dP = fmap1 G^T
+ *   layout 3: B element (k, n) at bm[((k/8)*ldb + n)*8 + k%8]   (ldb >= nc) -> grad_fmap1 = P G
+ * Batch strides are m*lda for a and k*ldb, nc*ldb, ceil(nc/8)*8*ldb, ceil(k/8)*8*ldb for bm
+ * (layouts 0-3); out is contiguous.  K may be
  * split over workgroups: then `workspace` must hold rmd_corr_grad_gemm_workspace_bytes() bytes
  * (0 = none needed) and a second pass sums the partial tiles in a fixed order (deterministic). */
 size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, int nc);

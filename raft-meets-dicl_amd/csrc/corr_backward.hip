@@ -11,17 +11,20 @@
 //     dfmap1[p]  = sum_l sum_t G_l[p, t] P_l[t]                         (GEMM, K = sum_l T_l)
 //     dP_l[t]    = sum_p G_l[p, t] fmap1[p]                              (GEMM, K = N)
 //     dfmap2     = sum_l unpool_l(dP_l) / sqrt(C)                        (this file)
-//   G (all levels, all lookups of a forward) is accumulated densely as (B, T, N) float32, query-minor
-//   like the forward pyramid: T = sum_l H_l W_l, level l's targets at row offset
-//   t_off[l] = sum_{l'<l} H_l' W_l', row-major (y, x) inside a level — a plain matrix, so both GEMMs
-//   are library GEMMs without transposes (dfmap1 = P^T G lands directly in (B, C, N)).
-//   rmd_corr_lookup_backward: lanes are consecutive queries, so a lane group whose (smooth) flow puts
-//   their patches on the same target row-column touches one contiguous 256-B run of G per access
-//   (the (B, N, T) layout made every wave access 64 different rows).  Each lane owns column (b, p)
-//   of G for its level: it spreads the (2r+1)^2 tap gradients over its (2r+2)^2 integer patch with
-//   the forward's bilinear weights (separable: x then y) and read-modify-writes the patch — no
-//   atomics: the patch rows are split over 3 lanes (parts) that write disjoint rows, no other lane
-//   touches column p, and successive lookups are ordered by the stream.
+//   G (all levels, all lookups of a forward) is accumulated densely in float32 in the forward
+//   pyramid's chunked query-minor order with 8-target chunks: target row (l, y) is cut into
+//   ceil(W_l / 8) chunks, chunk index ch = coff(l) + y * ceil(W_l / 8) + x / 8 over all levels, and
+//   element (b, t, p) sits at ((b * TC + ch) * N + p) * 8 + x % 8.  As a matrix over the padded
+//   targets t' = 8 ch + x % 8 (T' = 8 TC, pad columns stay zero) both GEMMs read it with 8-element
+//   blocked operand layouts (rmd_corr_grad_gemm layouts 2 / 3), so no transpose pass is needed.
+//   rmd_corr_lookup_backward: lanes are consecutive queries; at a tap, query p + 1's target is one
+//   column right of query p's (smooth flow), so in the chunked order 8 neighbouring lanes touch
+//   3 128-B lines (36-B lane stride) instead of 8 lines of the plain (B, T, N) order (N + 1 floats
+//   apart).  Each lane owns column (b, p) of G for its level: it spreads the (2r+1)^2 tap gradients
+//   over its (2r+2)^2 integer patch with the forward's bilinear weights (separable: x then y) and
+//   read-modify-writes the patch — no atomics: the patch rows are split over 3 lanes (parts) that
+//   write disjoint rows, no other lane touches column p, and successive lookups are ordered by the
+//   stream.
 
 #include "rmd_common.h"
 
@@ -30,13 +33,14 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__host__ __device__ inline long long level_targets(int h, int w, int l) { return (long long)(h >> l) * (w >> l); }
+constexpr int kGcw = 8;                // targets per G chunk
 
 struct GradGeom {
     int batch, height, width, levels;
     int lh[RMD_MAX_LEVELS], lw[RMD_MAX_LEVELS];
-    long long toff[RMD_MAX_LEVELS];   // column offset of level l inside a query row
-    long long T;                      // targets per query row (all levels)
+    int nch[RMD_MAX_LEVELS];          // chunks per target row of level l: ceil(W_l / 8)
+    long long coff[RMD_MAX_LEVELS];   // first chunk of level l
+    long long TC;                     // chunks per image (all levels); T' = 8 TC padded targets
 };
 
 inline GradGeom make_grad_geom(int batch, int h, int w, int levels) {
@@ -45,14 +49,15 @@ inline GradGeom make_grad_geom(int batch, int h, int w, int levels) {
     g.height = h;
     g.width = w;
     g.levels = levels;
-    long long t = 0;
+    long long c = 0;
     for (int l = 0; l < levels; ++l) {
         g.lh[l] = h >> l;
         g.lw[l] = w >> l;
-        g.toff[l] = t;
-        t += (long long)g.lh[l] * g.lw[l];
+        g.nch[l] = (g.lw[l] + kGcw - 1) / kGcw;
+        g.coff[l] = c;
+        c += (long long)g.lh[l] * g.nch[l];
     }
-    g.T = t;
+    g.TC = c;
     return g;
 }
 
@@ -83,7 +88,9 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
     const int xs = (int)fx0 - R, ys = (int)fy0 - R;
 
     const float* go = gout + ((size_t)b * g.levels + L) * D * D * (size_t)N + p;
-    float* col = grad + ((size_t)b * g.T + g.toff[L]) * (size_t)N + p;      // G[b][t_off + y*lw + x][p]
+    // G element (y, x) of this lane: chunk coff + y nch + x / 8, query p, slot x % 8
+    float* col = grad + (((size_t)b * g.TC + g.coff[L]) * N + p) * kGcw;
+    const size_t chs = (size_t)N * kGcw;                                       // one chunk step
 
     // x pass of tap row j: Q[j][i] = g[i][j](1-fx) + g[i-1][j] fx, i = 0..K-1 (zero for j outside 0..D-1)
     auto qrow = [&](int j, float (&q)[K]) {
@@ -110,11 +117,11 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
         qrow(j, qcur);
         const int y = ys + j;
         if (y >= 0 && y < lh) {
-            float* r = col + (size_t)y * lw * N;
+            float* r = col + (size_t)y * g.nch[L] * chs;
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 const int x = xs + i;
-                if (x >= 0 && x < lw) r[(size_t)x * N] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                if (x >= 0 && x < lw) r[(size_t)(x >> 3) * chs + (x & 7)] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
             }
         }
 #pragma unroll
@@ -122,30 +129,37 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
     }
 }
 
-// P (B, C, T) = avg-pooled fmap2 * scale, all levels; one thread per (b, c, t), t fastest: a wave
-// reads neighbouring target pixels of one channel plane (coalesced) and writes 256 B contiguous
+// P (B, C, T') = avg-pooled fmap2 * scale, all levels, in G's padded target order t' = 8 ch + x % 8
+// (pad targets x >= W_l are 0); one thread per (b, c, t'), t' fastest: a wave reads neighbouring
+// target pixels of one channel plane (coalesced) and writes 256 B contiguous
 __global__ void __launch_bounds__(kThreads)
 pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, float scale, float* __restrict__ P) {
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const long long total = (long long)g.batch * C * g.T;
+    const long long Tp = g.TC * kGcw;
+    const long long total = (long long)g.batch * C * Tp;
     if (idx >= total) return;
-    const long long t = idx % g.T;
-    const long long bc = idx / g.T;              // b * C + c: the channel plane
+    const long long t = idx % Tp;
+    const long long bc = idx / Tp;               // b * C + c: the channel plane
+    const long long ch = t / kGcw;
     int l = 0;
 #pragma unroll
     for (int k = 1; k < RMD_MAX_LEVELS; ++k)
-        if (k < g.levels && t >= g.toff[k]) l = k;
-    const int tl = (int)(t - g.toff[l]);
-    const int y = tl / g.lw[l], x = tl - y * g.lw[l];
-    const int s = 1 << l;
-    const float* src = f + (size_t)bc * g.height * g.width + (size_t)(y * s) * g.width + x * s;
+        if (k < g.levels && ch >= g.coff[k]) l = k;
+    const int cl = (int)(ch - g.coff[l]);
+    const int y = cl / g.nch[l], x = (cl - y * g.nch[l]) * kGcw + (int)(t % kGcw);
     float acc = 0.f;
-    for (int dy = 0; dy < s; ++dy)
-        for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.width + dx];
-    P[idx] = acc * (scale / (float)(s * s));
+    if (x < g.lw[l]) {
+        const int s = 1 << l;
+        const float* src = f + (size_t)bc * g.height * g.width + (size_t)(y * s) * g.width + x * s;
+        for (int dy = 0; dy < s; ++dy)
+            for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.width + dx];
+        acc *= scale / (float)(s * s);
+    }
+    P[idx] = acc;
 }
 
-// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T); one thread per output element
+// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T') in G's padded target order;
+// one thread per output element
 __global__ void __launch_bounds__(kThreads)
 unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float scale, float* __restrict__ df) {
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
@@ -155,14 +169,15 @@ unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float sca
     const int px = (int)(idx % HW);
     const long long bc = idx / HW;
     const int y = px / g.width, x = px - y * g.width;
-    const float* base = dP + (size_t)bc * g.T;
+    const float* base = dP + (size_t)bc * g.TC * kGcw;
     float acc = 0.f;
 #pragma unroll
     for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
         if (l >= g.levels) break;
         const int yl = y >> l, xl = x >> l;
         if (yl < g.lh[l] && xl < g.lw[l])
-            acc += base[g.toff[l] + (long long)yl * g.lw[l] + xl] * (1.0f / (float)(1 << (2 * l)));
+            acc += base[(g.coff[l] + (long long)yl * g.nch[l] + (xl >> 3)) * kGcw + (xl & 7)] *
+                   (1.0f / (float)(1 << (2 * l)));
     }
     df[idx] = acc * scale;
 }
@@ -180,9 +195,7 @@ int check_grad_args(int batch, int channels, int h, int w, int levels) {
 
 extern "C" long long rmd_corr_grad_targets(int height, int width, int levels) {
     if (height < 1 || width < 1 || levels < 1 || levels > RMD_MAX_LEVELS) return -1;
-    long long t = 0;
-    for (int l = 0; l < levels; ++l) t += rmd::level_targets(height, width, l);
-    return t;
+    return rmd::make_grad_geom(1, height, width, levels).TC * rmd::kGcw;
 }
 
 extern "C" int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* d, const float* coords,
@@ -212,7 +225,7 @@ extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels
     int rc = rmd::check_grad_args(batch, channels, height, width, levels);
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
-    const long long total = (long long)batch * channels * g.T;
+    const long long total = (long long)batch * channels * g.TC * rmd::kGcw;
     rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
                                rmd::as_stream(stream)>>>(fmap2, g, channels, scale, pooled);
     return rmd::check_launch("rmd_corr_pool_targets");

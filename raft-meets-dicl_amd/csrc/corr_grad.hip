@@ -4,8 +4,12 @@
 // fmap1^T fmap2 / sqrt(C), then avg_pool2d per level).  With the lookup backward's dense
 // query-minor gradient G (B, T, N) over the T pooled targets of all levels (corr_backward.hip) and
 // the pooled, scaled target features P (B, C, T), autograd of the matmul is
-//   dfmap1 = P . G           (B, C, N)   K = T        layout 0: G is K x Nc, n contiguous
-//   dP     = fmap1 . G^T     (B, C, T)   K = N        layout 1: G is Nc x K, k contiguous
+//   dfmap1 = P . G           (B, C, N)   K = T'       layout 3: G blocked along k (targets)
+//   dP     = fmap1 . G^T     (B, C, T')  K = N        layout 2: G blocked along n (targets)
+// B operand layouts (element (k, n), ldb = row stride):
+//   0: k * ldb + n (K x Nc, n contiguous)       1: n * ldb + k (Nc x K, k contiguous)
+//   2: ((n / 8) * ldb + k) * 8 + n % 8          3: ((k / 8) * ldb + n) * 8 + k % 8
+// (2 / 3 are the 8-target chunked order of the pyramid gradient G, corr_backward.hip)
 // (dP is then un-pooled onto dfmap2 by rmd_corr_unpool_targets).  Both run here in fp32 accuracy
 // as three bf16 MFMA products per k-step, x = hi + lo, hi = bf16(x), lo = bf16(x - hi):
 //   acc += A_lo.B_hi + A_hi.B_lo + A_hi.B_hi        (the dropped lo.lo term is ~2^-16 relative)
@@ -98,16 +102,18 @@ grad_gemm_x3(GemmArgs p) {
             const int row = m0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
             ra[it] = row < p.M ? load4<VA>(A + (size_t)row * p.lda, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if constexpr (LAYOUT == 0) {
+        if constexpr (LAYOUT == 0 || LAYOUT == 2) {
             // thread (kq, nq): k rows 4kq..4kq+3 of columns 4nq..4nq+3 — lanes (kq & 3, nq) of a wave
             // read 4 k rows x 256 contiguous bytes; waves 0-3 / 4-7 take column halves 0-63 / 64-127
+            // (layout 2: 4 consecutive n of one 8-block are contiguous too)
             const int kq = (lane & 3) | ((w & 3) << 2), n = n0 + 64 * (w >> 2) + 4 * (lane >> 2);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int k = k0 + 4 * kq + r;
                 rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (k < ke) {
-                    const float* src = Bm + (size_t)k * p.ldb;
+                    const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb
+                                                   : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7) - n;
                     if (VB && n + 3 < p.Nc) {
                         rb[r] = *reinterpret_cast<const float4*>(src + n);
                     } else {
@@ -122,7 +128,10 @@ grad_gemm_x3(GemmArgs p) {
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
                 const int row = n0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
-                rb[it] = row < p.Nc ? load4<VB>(Bm + (size_t)row * p.ldb, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
+                // layout 3: k..k+3 lie in one 8-block (k % 4 == 0), contiguous from the block's base
+                const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb
+                                               : Bm + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7) - k;
+                rb[it] = row < p.Nc ? load4<VB>(src, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
     };
@@ -135,7 +144,7 @@ grad_gemm_x3(GemmArgs p) {
             *reinterpret_cast<bf16x4*>(d) = hi;
             *reinterpret_cast<bf16x4*>(d + 128) = lo;
         }
-        if constexpr (LAYOUT == 0) {
+        if constexpr (LAYOUT == 0 || LAYOUT == 2) {
             // transpose: column 4nq + j of the thread's 4 k rows -> LDS row of that column, k offset 4kq
             const int kq = (lane & 3) | ((w & 3) << 2), nr = 64 * (w >> 2) + 4 * (lane >> 2);
             const float c0[4] = {rb[0].x, rb[1].x, rb[2].x, rb[3].x};
@@ -294,8 +303,9 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
                                   int k, int nc, int layout, float* out, void* workspace, void* stream) {
     RMD_REQUIRE(a && bm && out, RMD_ERR_ARG, "rmd_corr_grad_gemm: null pointer");
     RMD_REQUIRE(batch > 0 && m > 0 && k > 0 && nc > 0, RMD_ERR_SHAPE, "rmd_corr_grad_gemm: empty shape");
-    RMD_REQUIRE(layout == 0 || layout == 1, RMD_ERR_ARG, "rmd_corr_grad_gemm: layout must be 0 or 1");
-    RMD_REQUIRE(lda >= k && ldb >= (layout == 0 ? nc : k), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: bad row stride");
+    RMD_REQUIRE(layout >= 0 && layout <= 3, RMD_ERR_ARG, "rmd_corr_grad_gemm: layout must be 0..3");
+    RMD_REQUIRE(lda >= k && ldb >= (layout == 0 ? nc : layout == 3 ? nc : k), RMD_ERR_SHAPE,
+                "rmd_corr_grad_gemm: bad row stride");
     const rmd::Plan pl = rmd::plan(batch, m, k, nc);
     RMD_REQUIRE(pl.splits == 1 || workspace, RMD_ERR_ARG, "rmd_corr_grad_gemm: workspace required (%d splits)",
                 pl.splits);
@@ -307,7 +317,11 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     g.lda = lda;
     g.ldb = ldb;
     g.sa = (long long)m * lda;
-    g.sb = (layout == 0 ? (long long)k : (long long)nc) * ldb;
+    // batch stride of B: rows x ldb (layouts 0 / 1) or 8-blocks x 8 ldb (layouts 2 / 3)
+    g.sb = layout == 0 ? (long long)k * ldb
+         : layout == 1 ? (long long)nc * ldb
+         : layout == 2 ? (long long)((nc + 7) / 8) * 8 * ldb
+                       : (long long)((k + 7) / 8) * 8 * ldb;
     g.so = (long long)m * nc;
     g.M = m;
     g.K = k;
@@ -319,9 +333,14 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     g.ntn = pl.ntn;
     const long long nwg = (long long)pl.ntm * pl.ntn * pl.splits * batch;
     RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: grid too large");
-    const bool va = (lda & 3) == 0, vb = (ldb & 3) == 0;
+    const bool va = (lda & 3) == 0;
+    bool vb = (ldb & 3) == 0;
 #define RMD_GG(VA, VB)                                                                      \
-    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, st) : rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, st))
+    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, st)                             \
+     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, st)                           \
+     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, st)                           \
+                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, st))
+    if (layout >= 2) vb = true;                // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
     if (va && vb) RMD_GG(true, true);
     else if (va) RMD_GG(true, false);
     else if (vb) RMD_GG(false, true);

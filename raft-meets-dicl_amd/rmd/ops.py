@@ -154,10 +154,11 @@ def otf_lookup(st, coords, radius, mask_costs=()):
 #
 # The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an
 # input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
-# accumulates into ONE dense fp32 gradient G (B, T, N), query-minor, shared through _CorrState (include/rmd.h,
-# rmd_corr_lookup_backward); the pyramid backward then turns G into d fmap1 / d fmap2 with two plain
-# fp32 library GEMMs (hipBLASLt, no copies: G^T is a strided view) and the native pool / unpool
-# kernels (backward in fp32 in every precision mode).
+# accumulates into ONE dense fp32 gradient G over the T' padded targets, in the pyramid's chunked
+# query-minor order (8-target chunks, include/rmd.h, rmd_corr_lookup_backward), shared through
+# _CorrState; the pyramid backward then turns G into d fmap1 / d fmap2 with two split-bf16 MFMA GEMMs
+# that read G in its blocked order (rmd_corr_grad_gemm layouts 3 / 2, no transpose pass) and the
+# native pool / unpool kernels (backward in fp32 in every precision mode).
 
 class _CorrState:
     def __init__(self, pyr, f1, f2, precision):
@@ -202,16 +203,17 @@ class _CorrPyramidFn(torch.autograd.Function):
             stream = _stream(f1)
             _lib.check(lib.rmd_corr_pool_targets(_ptr(f2), b, c, h, w, levels, scale, _ptr(pooled), stream),
                        "rmd_corr_pool_targets")
-            G = st.grad.view(b, t, n)
+            G = st.grad                 # (B, T'/8, N, 8): element (t', p) at ((t'/8) N + p) 8 + t' % 8
             g1 = torch.empty((b, c, n), dtype=torch.float32, device=f1.device)
             dpool = torch.empty((b, c, t), dtype=torch.float32, device=f1.device)
             ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, c, t, n),
                                  lib.rmd_corr_grad_gemm_workspace_bytes(b, c, n, t), 1),
                              dtype=torch.uint8, device=f1.device)
-            # grad_fmap1 = P G (K = T), dP = fmap1 G^T (K = N): split-bf16 MFMA GEMMs (corr_grad.hip)
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 0, _ptr(g1), _ptr(ws),
+            # grad_fmap1 = P G (K = T', layout 3: G blocked along k), dP = fmap1 G^T (K = N, layout 2: G
+            # blocked along n): split-bf16 MFMA GEMMs (corr_grad.hip)
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, _ptr(g1), _ptr(ws),
                                               stream), "rmd_corr_grad_gemm")
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 1, _ptr(dpool), _ptr(ws),
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, _ptr(dpool), _ptr(ws),
                                               stream), "rmd_corr_grad_gemm")
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")

@@ -287,25 +287,45 @@ def test_dot_correlation_module_matches_reference_golden():
     assert rel_max_err(nodap.cpu().numpy(), g["out_nodap"]) < 1e-4
 
 
-@pytest.mark.parametrize("layout", [0, 1])
+def _gemm_operand(bl, layout):
+    """Storage of the logical B operand bl (b, k, nc) in rmd_corr_grad_gemm layout 0-3 (include/rmd.h)
+    and its ldb."""
+    b, k, nc = bl.shape
+    if layout == 0:
+        return bl.contiguous(), nc
+    if layout == 1:
+        return bl.transpose(1, 2).contiguous(), k
+    if layout == 2:                                  # ((n/8) ldb + k) 8 + n%8, ldb = k
+        npad = (nc + 7) // 8 * 8
+        t = torch.zeros(b, k, npad)
+        t[:, :, :nc] = bl
+        return t.view(b, k, npad // 8, 8).permute(0, 2, 1, 3).contiguous(), k
+    kpad = (k + 7) // 8 * 8                          # layout 3: ((k/8) ldb + n) 8 + k%8, ldb = nc
+    t = torch.zeros(b, kpad, nc)
+    t[:, :k] = bl
+    return t.view(b, kpad // 8, 8, nc).permute(0, 1, 3, 2).contiguous(), nc
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
 @pytest.mark.parametrize("b,m,k,nc", [(6, 256, 3790, 2852), (2, 100, 37, 45), (1, 300, 129, 130), (3, 32, 1000, 7)])
 def test_corr_grad_gemm_vs_fp64(layout, b, m, k, nc):
-    """rmd_corr_grad_gemm (split-bf16 x3 MFMA) against a float64 GEMM, elementwise.  Shapes: the cfg5
-    backward (B6, C256, T = 3790 pooled targets, N = 2852 queries; lda = 3790 is not 16-B aligned), ragged
-    tiles, M over two 256-row tiles, a K split into several workgroups."""
+    """rmd_corr_grad_gemm (split-bf16 x3 MFMA) against a float64 GEMM, elementwise, in all four B
+    layouts (2 / 3: the 8-target blocked order of the pyramid gradient).  Shapes: the cfg5 backward
+    (B6, C256, T = 3790 pooled targets, N = 2852 queries; lda = 3790 is not 16-B aligned), ragged
+    tiles and 8-blocks, M over two 256-row tiles, a K split into several workgroups."""
     import ctypes
     from rmd import _lib
     g = torch.Generator(device="cpu").manual_seed(m + k)
     a = torch.randn(b, m, k, generator=g)
-    bm = torch.randn(b, k, nc, generator=g) if layout == 0 else torch.randn(b, nc, k, generator=g)
-    ref = torch.bmm(a.double(), bm.double() if layout == 0 else bm.double().transpose(1, 2))
+    bl = torch.randn(b, k, nc, generator=g)
+    ref = torch.bmm(a.double(), bl.double())
+    bm, ldb = _gemm_operand(bl, layout)
     lib = _lib.lib()
     ad, bd = a.to(DEV), bm.to(DEV)
     out = torch.full((b, m, nc), float("nan"), device=DEV)
     ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, m, k, nc), 1), dtype=torch.uint8, device=DEV)
-    rc = lib.rmd_corr_grad_gemm(ctypes.c_void_p(ad.data_ptr()), k, ctypes.c_void_p(bd.data_ptr()),
-                                nc if layout == 0 else k, b, m, k, nc, layout, ctypes.c_void_p(out.data_ptr()),
-                                ctypes.c_void_p(ws.data_ptr()), None)
+    rc = lib.rmd_corr_grad_gemm(ctypes.c_void_p(ad.data_ptr()), k, ctypes.c_void_p(bd.data_ptr()), ldb, b, m, k, nc,
+                                layout, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), None)
     assert rc == 0
     torch.cuda.synchronize()
     got = out.cpu().double()
