@@ -130,32 +130,34 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
 }
 
 // P (B, C, T') = avg-pooled fmap2 * scale, all levels, in G's padded target order t' = 8 ch + x % 8
-// (pad targets x >= W_l are 0); one thread per (b, c, t'), t' fastest: a wave reads neighbouring
-// target pixels of one channel plane (coalesced) and writes 256 B contiguous
+// (pad targets x >= W_l are 0), one launch per level: level 0 is fmap2 * scale, level l the 2x2
+// average of level l - 1 in P (avg_pool2d(k=2, s=2) of the previous level, raft.py:45-46, floor
+// sizes: every 2x2 window of level l - 1 exists).  One thread per (b, c, level-l target), x fastest
+// within a chunk row: a wave reads and writes contiguous runs.
 __global__ void __launch_bounds__(kThreads)
-pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, float scale, float* __restrict__ P) {
+pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, int l, float scale, float* __restrict__ P) {
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const long long Tp = g.TC * kGcw;
-    const long long total = (long long)g.batch * C * Tp;
+    const long long per = (long long)g.lh[l] * g.nch[l] * kGcw;         // padded targets of level l
+    const long long total = (long long)g.batch * C * per;
     if (idx >= total) return;
-    const long long t = idx % Tp;
-    const long long bc = idx / Tp;               // b * C + c: the channel plane
-    const long long ch = t / kGcw;
-    int l = 0;
-#pragma unroll
-    for (int k = 1; k < RMD_MAX_LEVELS; ++k)
-        if (k < g.levels && ch >= g.coff[k]) l = k;
-    const int cl = (int)(ch - g.coff[l]);
-    const int y = cl / g.nch[l], x = (cl - y * g.nch[l]) * kGcw + (int)(t % kGcw);
-    float acc = 0.f;
+    const long long bc = idx / per;
+    const int tl = (int)(idx - bc * per);
+    const int y = tl / (g.nch[l] * kGcw), x = tl - y * g.nch[l] * kGcw;
+    const long long Tp = g.TC * kGcw;
+    float v = 0.f;
     if (x < g.lw[l]) {
-        const int s = 1 << l;
-        const float* src = f + (size_t)bc * g.height * g.width + (size_t)(y * s) * g.width + x * s;
-        for (int dy = 0; dy < s; ++dy)
-            for (int dx = 0; dx < s; ++dx) acc += src[(size_t)dy * g.width + dx];
-        acc *= scale / (float)(s * s);
+        if (l == 0) {
+            v = f[(size_t)bc * g.height * g.width + (size_t)y * g.width + x] * scale;
+        } else {
+            const float* q = P + (size_t)bc * Tp;
+            const int pl = l - 1, np = g.nch[pl];
+            auto at = [&](int yy, int xx) {
+                return q[(g.coff[pl] + (long long)yy * np + (xx >> 3)) * kGcw + (xx & 7)];
+            };
+            v = (at(2 * y, 2 * x) + at(2 * y, 2 * x + 1) + at(2 * y + 1, 2 * x) + at(2 * y + 1, 2 * x + 1)) * 0.25f;
+        }
     }
-    P[idx] = acc;
+    P[(size_t)bc * Tp + g.coff[l] * kGcw + tl] = v;
 }
 
 // dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T') in G's padded target order;
@@ -225,9 +227,11 @@ extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels
     int rc = rmd::check_grad_args(batch, channels, height, width, levels);
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
-    const long long total = (long long)batch * channels * g.TC * rmd::kGcw;
-    rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
-                               rmd::as_stream(stream)>>>(fmap2, g, channels, scale, pooled);
+    for (int l = 0; l < levels; ++l) {          // level l reads level l - 1 (same stream: ordered)
+        const long long total = (long long)batch * channels * g.lh[l] * g.nch[l] * rmd::kGcw;
+        rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
+                                   rmd::as_stream(stream)>>>(fmap2, g, channels, l, scale, pooled);
+    }
     return rmd::check_launch("rmd_corr_pool_targets");
 }
 
