@@ -60,15 +60,16 @@ __device__ __forceinline__ void split4(float a, float b, float c, float d, bf16x
     lo[3] = (__bf16)(d - (float)hi[3]);
 }
 
-// 4 consecutive elements of a row starting at column k (row valid, k < kend checked per element)
+// the 4 consecutive elements k .. k + 3 at `at` (the address of element k; row valid, k < kend
+// checked per element)
 template <bool VEC>
-__device__ __forceinline__ float4 load4(const float* __restrict__ row, int k, int kend) {
-    if (VEC && k + 3 < kend) return *reinterpret_cast<const float4*>(row + k);
+__device__ __forceinline__ float4 load4(const float* __restrict__ at, int k, int kend) {
+    if (VEC && k + 3 < kend) return *reinterpret_cast<const float4*>(at);
     float4 v;
-    v.x = k + 0 < kend ? row[k + 0] : 0.f;
-    v.y = k + 1 < kend ? row[k + 1] : 0.f;
-    v.z = k + 2 < kend ? row[k + 2] : 0.f;
-    v.w = k + 3 < kend ? row[k + 3] : 0.f;
+    v.x = k + 0 < kend ? at[0] : 0.f;
+    v.y = k + 1 < kend ? at[1] : 0.f;
+    v.z = k + 2 < kend ? at[2] : 0.f;
+    v.w = k + 3 < kend ? at[3] : 0.f;
     return v;
 }
 
@@ -100,7 +101,7 @@ grad_gemm_x3(GemmArgs p) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
             const int row = m0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
-            ra[it] = row < p.M ? load4<VA>(A + (size_t)row * p.lda, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
+            ra[it] = row < p.M ? load4<VA>(A + (size_t)row * p.lda + k, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if constexpr (LAYOUT == 0 || LAYOUT == 2) {
             // thread (kq, nq): k rows 4kq..4kq+3 of columns 4nq..4nq+3 — lanes (kq & 3, nq) of a wave
@@ -112,15 +113,16 @@ grad_gemm_x3(GemmArgs p) {
                 const int k = k0 + 4 * kq + r;
                 rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (k < ke) {
-                    const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb
-                                                   : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7) - n;
+                    // address of element (k, n); n .. n + 3 follow it contiguously in both layouts
+                    const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb + n
+                                                   : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
                     if (VB && n + 3 < p.Nc) {
-                        rb[r] = *reinterpret_cast<const float4*>(src + n);
+                        rb[r] = *reinterpret_cast<const float4*>(src);
                     } else {
-                        rb[r].x = n + 0 < p.Nc ? src[n + 0] : 0.f;
-                        rb[r].y = n + 1 < p.Nc ? src[n + 1] : 0.f;
-                        rb[r].z = n + 2 < p.Nc ? src[n + 2] : 0.f;
-                        rb[r].w = n + 3 < p.Nc ? src[n + 3] : 0.f;
+                        rb[r].x = n + 0 < p.Nc ? src[0] : 0.f;
+                        rb[r].y = n + 1 < p.Nc ? src[1] : 0.f;
+                        rb[r].z = n + 2 < p.Nc ? src[2] : 0.f;
+                        rb[r].w = n + 3 < p.Nc ? src[3] : 0.f;
                     }
                 }
             }
@@ -128,9 +130,9 @@ grad_gemm_x3(GemmArgs p) {
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
                 const int row = n0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
-                // layout 3: k..k+3 lie in one 8-block (k % 4 == 0), contiguous from the block's base
-                const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb
-                                               : Bm + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7) - k;
+                // layout 3: k .. k + 3 lie in one 8-block (k % 4 == 0), contiguous like layout 1's row
+                const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb + k
+                                               : Bm + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7);
                 rb[it] = row < p.Nc ? load4<VB>(src, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }

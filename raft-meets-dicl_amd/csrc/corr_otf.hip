@@ -34,6 +34,9 @@ constexpr int kBX = 16, kBY = 2, kQ = kBX * kBY;     // query block = 2 query se
 #endif
 constexpr int kMaxT = RMD_OTF_MAXT;                  // targets of one band
 constexpr int kLd = kMaxT + 5;                       // S row stride (spreads queries over banks)
+// diagnostic variant (RMD_OTF_PF=1): the next band task's target fragments in flight during this task's
+// MFMAs; needs 256 VGPRs (2 waves/SIMD, spills) and measured slower: 123 vs 100 us at cfg2 bf16
+// (profiles/otf_ablate_r02.json)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -174,17 +177,19 @@ __device__ __forceinline__ float seg_elem(const T* segbase, int i, int c) {
 // run on the same XCD and share its L2.  One block runs every level of its 32 queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, int R, int CPT>
-__global__ void __launch_bounds__(kLookThreads)
+template <typename T, int R, int CPT, bool PF>
+__global__ void __launch_bounds__(kLookThreads, PF ? 2 : 1)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out, int ablate) {
     using SG = Seg<T>;
     using frag = typename SG::frag;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K;
     extern __shared__ float S[];                       // [kQ][kLd]: band (boxed) or patch (per query)
-    __shared__ int box[4];                             // x0, x1, y0, y1 (min / max)
-    __shared__ int sxs[kQ], sys[kQ];
-    __shared__ float sfx[kQ], sfy[kQ];
+    // every level's window origins / fractions and the block's bounding box per level, computed once
+    // before the level loop (no per-level reduction barriers)
+    __shared__ int box[RMD_MAX_LEVELS][4];             // x0, x1, y0, y1 (min / max)
+    __shared__ int sxs[RMD_MAX_LEVELS][kQ], sys[RMD_MAX_LEVELS][kQ];
+    __shared__ float sfx[RMD_MAX_LEVELS][kQ], sfy[RMD_MAX_LEVELS][kQ];
     const int nbx = (g.W + kBX - 1) / kBX, nqb = nbx * ((g.H + kBY - 1) / kBY);
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -213,12 +218,16 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             dst[QV + v] = s1[v];
         }
     }
+    // thread (level tid / kQ, query tid % kQ)
     float cx0 = 0.f, cy0 = 0.f;
-    if (tid < kQ) {
-        const int y = min(qy0 + tid / kBX, g.H - 1), x = min(qx0 + tid % kBX, g.W - 1);
+    if (tid < kQ * g.L) {
+        const int q = tid % kQ;
+        const int y = min(qy0 + q / kBX, g.H - 1), x = min(qx0 + q % kBX, g.W - 1);
         cx0 = coords[((size_t)b * 2 + 0) * N + y * g.W + x];
         cy0 = coords[((size_t)b * 2 + 1) * N + y * g.W + x];
     }
+    static_assert(kQ * RMD_MAX_LEVELS <= kLookThreads, "one thread per (level, query)");
+    if (tid < RMD_MAX_LEVELS * 4) box[tid >> 2][tid & 3] = (tid & 1) ? -(1 << 30) : (1 << 30);
     __syncthreads();
     frag q0[NLS], q1[NLS];
     if constexpr (CPT > 0) {
@@ -229,6 +238,25 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             q1[ls] = qs[(NLS + ls) * 64 + lane];
         }
     }
+    if (tid < kQ * g.L) {
+        // query's window origin at level L (coords clamped as rmd_corr_lookup does)
+        const int q = tid % kQ, L = tid / kQ;
+        const float inv = 1.0f / (float)(1 << L);
+        const float rx = cx0 * inv, ry = cy0 * inv;
+        const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f);
+        const float cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
+        const float fx0 = floorf(cx), fy0 = floorf(cy);
+        const int xs = (int)fx0 - R, ys = (int)fy0 - R;
+        sxs[L][q] = xs;
+        sys[L][q] = ys;
+        sfx[L][q] = rx - floorf(rx);                // NaN / inf coordinate -> NaN window (grid_sample)
+        sfy[L][q] = ry - floorf(ry);
+        atomicMin(&box[L][0], xs);
+        atomicMax(&box[L][1], xs + K - 1);
+        atomicMin(&box[L][2], ys);
+        atomicMax(&box[L][3], ys + K - 1);
+    }
+    __syncthreads();                                   // boxes complete; the query fragments are read: S is free
     // thread items (q, a): query q, window x-offset a; hx[i][jj] = row jj of the window, x-interpolated
     constexpr int ITEMS = (kQ * D + kLookThreads - 1) / kLookThreads;
 
@@ -246,33 +274,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             }
             continue;
         }
-        if (tid == 0) {
-            box[0] = 1 << 30;
-            box[1] = -(1 << 30);
-            box[2] = 1 << 30;
-            box[3] = -(1 << 30);
-        }
-        __syncthreads();                               // also: S / box of the previous level are free
-        if (tid < kQ) {
-            // query's window origin at level L (coords clamped as rmd_corr_lookup does)
-            const float inv = 1.0f / (float)(1 << L);
-            const float rx = cx0 * inv, ry = cy0 * inv;
-            const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f);
-            const float cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
-            const float fx0 = floorf(cx), fy0 = floorf(cy);
-            const int xs = (int)fx0 - R, ys = (int)fy0 - R;
-            sxs[tid] = xs;
-            sys[tid] = ys;
-            sfx[tid] = rx - floorf(rx);                // NaN / inf coordinate -> NaN window (grid_sample)
-            sfy[tid] = ry - floorf(ry);
-            atomicMin(&box[0], xs);
-            atomicMax(&box[1], xs + K - 1);
-            atomicMin(&box[2], ys);
-            atomicMax(&box[3], ys + K - 1);
-        }
-        __syncthreads();
-        const int bx0 = max(box[0], 0), bx1 = min(box[1], lw - 1);
-        const int by0 = max(box[2], 0), by1 = min(box[3], lh - 1);
+        const int bx0 = max(box[L][0], 0), bx1 = min(box[L][1], lw - 1);
+        const int by0 = max(box[L][2], 0), by1 = min(box[L][3], lh - 1);
         const int th = max(by1 - by0 + 1, 0);
         const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0, sw = nseg * 16;
         const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
@@ -301,19 +304,29 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                            (size_t)lane * SG::LE;
                 };
                 if constexpr (CPT > 0) {
-                    for (int task = w; task < ntask; task += kWaves) {
-                        if (ablate & 2) break;
+                    // the next task's target fragments load while this task's MFMAs run
+                    auto tload = [&](frag (&t)[NLS], int task) {
                         const T* tsb = tptr(task);
-                        frag t[NLS];
 #pragma unroll
                         for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                    };
+                    frag tc[NLS], tn[NLS];
+                    if (PF && w < ntask && !(ablate & 2)) tload(tc, w);
+                    for (int task = w; task < ntask; task += kWaves) {
+                        if (ablate & 2) break;
+                        if (!PF) tload(tc, task);
+                        else if (task + kWaves < ntask) tload(tn, task + kWaves);
                         f32x4 a0 = {}, a1 = {};
 #pragma unroll
                         for (int ls = 0; ls < NLS; ++ls) {
-                            SG::mma(a0, t[ls], q0[ls]);
-                            SG::mma(a1, t[ls], q1[ls]);
+                            SG::mma(a0, tc[ls], q0[ls]);
+                            SG::mma(a1, tc[ls], q1[ls]);
                         }
                         store(a0, a1, task);
+                        if (PF) {
+#pragma unroll
+                            for (int ls = 0; ls < NLS; ++ls) tc[ls] = tn[ls];
+                        }
                     }
                 } else {
                     for (int task = w; task < ntask; task += kWaves) {
@@ -335,8 +348,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     const int idx = tid + i * kLookThreads;
                     if (idx >= kQ * D) break;
                     const int q = idx % kQ, a = idx / kQ;
-                    const int xs = sxs[q], ys = sys[q];
-                    const float fx = sfx[q];
+                    const int xs = sxs[L][q], ys = sys[L][q];
+                    const float fx = sfx[L][q];
                     const float* Sq = S + q * kLd;
 #pragma unroll
                     for (int jj = 0; jj < K; ++jj) {
@@ -358,7 +371,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             // box wider than kMaxT: each query's own (2r+2)^2 patch, one dot product per thread
             for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
                 const int q = idx / KK, r = idx - q * KK;
-                const int ty = sys[q] + r / K, tx = sxs[q] + r % K;
+                const int ty = sys[L][q] + r / K, tx = sxs[L][q] + r % K;
                 float acc = 0.f;
                 if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
                     const T* qs = q < kBX ? qsb : qsb1;
@@ -373,11 +386,12 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 const int idx = tid + i * kLookThreads;
                 if (idx >= kQ * D) break;
                 const int q = idx % kQ, a = idx / kQ;
-                const float fx = sfx[q];
+                const float fx = sfx[L][q];
                 const float* Sq = S + q * kLd;
 #pragma unroll
                 for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Sq[jj * K + a + 1] - Sq[jj * K + a], Sq[jj * K + a]);
             }
+            __syncthreads();                           // S is free for the next level
         }
 
         // y-interpolation and the (a, b)-major output planes
@@ -388,7 +402,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             const int q = idx % kQ, a = idx / kQ;
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y >= g.H || x >= g.W) continue;
-            const float fy = sfy[q] + (sfx[q] - sfx[q]);   // a NaN x weight reaches rows outside the band too
+            const float fy = sfy[L][q] + (sfx[L][q] - sfx[L][q]);   // a NaN x weight reaches rows outside the band too
             if (ablate & 1) {
                 if (hx[i][0] == 123.f) ob[0] = fy;       // keep the sums live
                 continue;
@@ -480,10 +494,16 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     // phase
     const int ablate = env_knob("RMD_OTF_ABLATE", 0);           // always 0 outside librmd_diag.so
     const bool force_rt = env_knob("RMD_OTF_RUNTIME", 0) != 0;
+#ifdef RMD_DIAG
+    const bool pf = env_knob("RMD_OTF_PF", 0) != 0;
+#define RMD_OTF_K(T, RR, CC) (pf ? otf_lookup_kernel<T, RR, CC, true> : otf_lookup_kernel<T, RR, CC, false>)
+#else
+#define RMD_OTF_K(T, RR, CC) otf_lookup_kernel<T, RR, CC, false>
+#endif
     const int cpt = force_rt || (compute == RMD_F32 && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
 #define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \
-        auto k = otf_lookup_kernel<T, RR, CC>;                                                                 \
+        auto k = RMD_OTF_K(T, RR, CC);                                                                         \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
@@ -516,5 +536,6 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #undef RMD_OTF_R
 #undef RMD_OTF_C
 #undef RMD_OTF
+#undef RMD_OTF_K
     return check_launch("rmd_corr_otf_lookup");
 }
