@@ -53,6 +53,7 @@ CASES = [
     (1, 16, 30, 50, 2, 7, 25.0, ()),           # huge spread: union boxes span many bands
     (1, 256, 46, 62, 4, 4, 4.0, (3, 6)),       # cfg1 feature shape, levels 0 and 3 masked
     (1, 8, 9, 70, 1, 1, 0.5, ()),              # one level, r=1, wide map
+    (1, 320, 14, 20, 3, 3, 2.0, ()),           # C > 256: runtime-channel path (Cp 384: 12 bf16 / 24 f32 load steps)
 ]
 
 
