@@ -132,56 +132,54 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
 // P (B, C, T') = avg-pooled fmap2 * scale, all levels, in G's padded target order t' = 8 ch + x % 8
 // (pad targets x >= W_l are 0), one launch per level: level 0 is fmap2 * scale, level l the 2x2
 // average of level l - 1 in P (avg_pool2d(k=2, s=2) of the previous level, raft.py:45-46, floor
-// sizes: every 2x2 window of level l - 1 exists).  One thread per (b, c, level-l target), x fastest
-// within a chunk row: a wave reads and writes contiguous runs.
+// sizes: every 2x2 window of level l - 1 exists).  grid (level-l padded targets / 256, B * C): one
+// thread per (b, c, target), x fastest within a chunk row (a wave reads and writes contiguous runs;
+// 32-bit index math only).
 __global__ void __launch_bounds__(kThreads)
-pool_targets_kernel(const float* __restrict__ f, GradGeom g, int C, int l, float scale, float* __restrict__ P) {
-    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const long long per = (long long)g.lh[l] * g.nch[l] * kGcw;         // padded targets of level l
-    const long long total = (long long)g.batch * C * per;
-    if (idx >= total) return;
-    const long long bc = idx / per;
-    const int tl = (int)(idx - bc * per);
-    const int y = tl / (g.nch[l] * kGcw), x = tl - y * g.nch[l] * kGcw;
-    const long long Tp = g.TC * kGcw;
+pool_targets_kernel(const float* __restrict__ f, GradGeom g, int l, float scale, float* __restrict__ P) {
+    const int per = g.lh[l] * g.nch[l] * kGcw;                    // padded targets of level l
+    const int tl = blockIdx.x * kThreads + threadIdx.x;
+    if (tl >= per) return;
+    const size_t bc = blockIdx.y;
+    const int rowp = g.nch[l] * kGcw;
+    const int y = tl / rowp, x = tl - y * rowp;
+    const size_t Tp = (size_t)g.TC * kGcw;
     float v = 0.f;
     if (x < g.lw[l]) {
         if (l == 0) {
-            v = f[(size_t)bc * g.height * g.width + (size_t)y * g.width + x] * scale;
+            v = f[bc * g.height * g.width + (size_t)y * g.width + x] * scale;
         } else {
-            const float* q = P + (size_t)bc * Tp;
+            const float* q = P + bc * Tp;
             const int pl = l - 1, np = g.nch[pl];
             auto at = [&](int yy, int xx) {
-                return q[(g.coff[pl] + (long long)yy * np + (xx >> 3)) * kGcw + (xx & 7)];
+                return q[(size_t)(g.coff[pl] + (long long)yy * np + (xx >> 3)) * kGcw + (xx & 7)];
             };
             v = (at(2 * y, 2 * x) + at(2 * y, 2 * x + 1) + at(2 * y + 1, 2 * x) + at(2 * y + 1, 2 * x + 1)) * 0.25f;
         }
     }
-    P[(size_t)bc * Tp + g.coff[l] * kGcw + tl] = v;
+    P[bc * Tp + (size_t)g.coff[l] * kGcw + tl] = v;
 }
 
-// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T') in G's padded target order;
-// one thread per output element
+// dfmap2 (B, C, H, W) = sum_l unpool_l(dP_l) * scale / 4^l, dP (B, C, T') in G's padded target order.
+// grid (H W / 256, B * C): one thread per output element, 32-bit index math only.
 __global__ void __launch_bounds__(kThreads)
-unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, int C, float scale, float* __restrict__ df) {
-    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+unpool_targets_kernel(const float* __restrict__ dP, GradGeom g, float scale, float* __restrict__ df) {
     const int HW = g.height * g.width;
-    const long long total = (long long)g.batch * C * HW;
-    if (idx >= total) return;
-    const int px = (int)(idx % HW);
-    const long long bc = idx / HW;
+    const int px = blockIdx.x * kThreads + threadIdx.x;
+    if (px >= HW) return;
+    const size_t bc = blockIdx.y;
     const int y = px / g.width, x = px - y * g.width;
-    const float* base = dP + (size_t)bc * g.TC * kGcw;
+    const float* base = dP + bc * (size_t)g.TC * kGcw;
     float acc = 0.f;
 #pragma unroll
     for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
         if (l >= g.levels) break;
         const int yl = y >> l, xl = x >> l;
         if (yl < g.lh[l] && xl < g.lw[l])
-            acc += base[(g.coff[l] + (long long)yl * g.nch[l] + (xl >> 3)) * kGcw + (xl & 7)] *
+            acc += base[(size_t)(g.coff[l] + (long long)yl * g.nch[l] + (xl >> 3)) * kGcw + (xl & 7)] *
                    (1.0f / (float)(1 << (2 * l)));
     }
-    df[idx] = acc * scale;
+    df[bc * HW + px] = acc * scale;
 }
 
 int check_grad_args(int batch, int channels, int h, int w, int levels) {
@@ -227,10 +225,11 @@ extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels
     int rc = rmd::check_grad_args(batch, channels, height, width, levels);
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
+    RMD_REQUIRE((long long)batch * channels <= 65535, RMD_ERR_SHAPE, "rmd_corr_pool_targets: batch * channels > 65535");
     for (int l = 0; l < levels; ++l) {          // level l reads level l - 1 (same stream: ordered)
-        const long long total = (long long)batch * channels * g.lh[l] * g.nch[l] * rmd::kGcw;
-        rmd::pool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
-                                   rmd::as_stream(stream)>>>(fmap2, g, channels, l, scale, pooled);
+        const int per = g.lh[l] * g.nch[l] * rmd::kGcw;
+        const dim3 grid((per + rmd::kThreads - 1) / rmd::kThreads, batch * channels);
+        rmd::pool_targets_kernel<<<grid, rmd::kThreads, 0, rmd::as_stream(stream)>>>(fmap2, g, l, scale, pooled);
     }
     return rmd::check_launch("rmd_corr_pool_targets");
 }
@@ -241,9 +240,9 @@ extern "C" int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int 
     int rc = rmd::check_grad_args(batch, channels, height, width, levels);
     if (rc) return rc;
     const rmd::GradGeom g = rmd::make_grad_geom(batch, height, width, levels);
-    const long long total = (long long)batch * channels * height * width;
-    rmd::unpool_targets_kernel<<<(unsigned)((total + rmd::kThreads - 1) / rmd::kThreads), rmd::kThreads, 0,
-                                 rmd::as_stream(stream)>>>(grad_pooled, g, channels, scale, grad_fmap2);
+    RMD_REQUIRE((long long)batch * channels <= 65535, RMD_ERR_SHAPE, "rmd_corr_unpool_targets: batch * channels > 65535");
+    const dim3 grid((height * width + rmd::kThreads - 1) / rmd::kThreads, batch * channels);
+    rmd::unpool_targets_kernel<<<grid, rmd::kThreads, 0, rmd::as_stream(stream)>>>(grad_pooled, g, scale, grad_fmap2);
     return rmd::check_launch("rmd_corr_unpool_targets");
 }
 
