@@ -249,8 +249,9 @@ def train_leg(args, world, rank, device):
         sched.step()
         return loss
 
-    for _ in range(args.train_warmup):
+    for i in range(args.train_warmup):
         step()
+        progress(rank, f"train_step warm-up {i + 1}/{args.train_warmup}")
     torch.cuda.synchronize(device)
     if world > 1:
         torch.distributed.barrier()
@@ -306,8 +307,9 @@ def hybrid_leg(args, world, rank, device):
         i1s.append(i1), i2s.append(i2)
     img1, img2 = (torch.from_numpy(np.concatenate(x)).to(device) for x in (i1s, i2s))
     with torch.no_grad():
-        for _ in range(args.hybrid_warmup):
+        for i in range(args.hybrid_warmup):
             net(img1, img2, (4, 3, 3))
+            progress(rank, f"hybrid_inference warm-up {i + 1}/{args.hybrid_warmup}")
         torch.cuda.synchronize(device)
         if world > 1:
             torch.distributed.barrier()
@@ -407,6 +409,12 @@ def dicl_leg(args, world, rank, device):
             "displacement_range": list(md), "channels": c, "finite": fin,
             "scaling": "strong" if args.global_batch else "weak", "dtype": "fp32",
             "data": "synthetic feature maps (encoder / context nets outside the hot path)"}
+
+
+def progress(rank, what):
+    """One stderr line per leg and rank (the JSON line stays the only stdout output): shows where a
+    long multi-rank run is."""
+    print(f"[bench] rank {rank} {time.strftime('%H:%M:%S')} {what}", file=sys.stderr, flush=True)
 
 
 def job_time(elapsed, world, device):
@@ -581,7 +589,9 @@ def main():
         res["roofline"] = roof_gemm if dominant_gemm else roof_look
         res["roofline_gemm"] = roof_gemm
         res["roofline_lookup"] = roof_look
+        progress(rank, "headline leg done")
         if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
+            progress(rank, "model_level leg")
             res["model_level"] = model_level(device, args.precision)
         # extra legs run on every rank (batch shards / DDP collectives); a Python-level failure in one
         # (raised symmetrically on every rank, e.g. out of memory) is recorded instead of losing the
@@ -590,6 +600,7 @@ def main():
                                (args.train, "train_step", train_leg)):
             if flag != "on":
                 continue
+            progress(rank, f"{key} leg")
             try:
                 out = leg(args, world, rank, device)
             except Exception as e:                      # noqa: BLE001 — reported in the JSON line
@@ -599,6 +610,7 @@ def main():
                 res[key] = out
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
+            progress(rank, "cpu_baseline leg")
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)
     if world > 1:
