@@ -267,7 +267,9 @@ int rmd_dicl_stack_int_warped_backward(const float* grad_mvol, const float* fmap
  * W = conv1.weight[:,:,0,0] (D x D).  Replaces DisplacementAwareProjection.forward
  * (src/models/common/blocks/dicl.py:143-150), the per-level DAPs of raft.py:146-168 and the
  * 324x324 'full' DAP of raft_dicl_ml.py:268-273,339-341.  transpose = 1 applies W^T (the input
- * gradient).  x, out: (B, D, pixels) float32.
+ * gradient).  x, out: (B, D, pixels) float32.  Computed as a split-bf16 MFMA GEMM (W and x split
+ * into hi + lo bf16, W_lo.x_hi + W_hi.x_lo + W_hi.x_hi accumulated in fp32: ~1.5e-5 of float64)
+ * for D <= 1024; larger D falls back to an exact-fp32 VALU kernel.
  */
 int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose, float* out,
             void* stream);
