@@ -179,3 +179,41 @@ def test_bench_rejects_world_size_mismatch():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run",
                           "--no-cpu-baseline"], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
+
+
+def _rccl_worker(port, q):
+    """One rank on the RCCL ("nccl") backend: process-group init, an all_reduce and a DDP step through the
+    correlation autograd on cuda:0 (RCCL cannot put two ranks on one GPU, so the 1-GPU box exercises
+    the backend itself; the N-rank data path is the gloo test above and the driver's 8-GPU bench)."""
+    sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        t = torch.full((4,), 2.0, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        net = torch.nn.parallel.DistributedDataParallel(_TinyCorrNet().to(dev), device_ids=[0])
+        img1, img2, co = (x.to(dev) for x in _inputs(4, 10))
+        net(img1, img2, co).backward()
+        q.put((dist.get_backend(), float(t.sum()), net.module.enc.weight.grad.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_backend_ddp_step_one_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    backend, s, gw = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl" and s == 8.0
+    sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+    dev = torch.device("cuda", 0)
+    net = _TinyCorrNet().to(dev)
+    img1, img2, co = (x.to(dev) for x in _inputs(4, 10))
+    net(img1, img2, co).backward()
+    np.testing.assert_allclose(gw, net.enc.weight.grad.cpu().numpy(), rtol=1e-5, atol=1e-7)
