@@ -676,6 +676,155 @@ dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __re
     }
 }
 
+// Same backward, 2 pixels per lane, with a GENERAL merge of the lane's two patches: whenever the
+// pixels' integer window origins differ by at most 1 row and 2 columns (any smooth flow), the two
+// (2r+2)^2 patches are summed in registers over their joint box of (2r+3) rows x (2r+4) columns and
+// every lane adds one run of 2r+4 values per joint row.  backward4 merges only origins exactly one
+// column apart and sends every other lane through a per-pixel path of 2 (2r+2) adds per row; because
+// a wave executes every path one of its lanes takes, a wave with both kinds paid for both (the
+// cost of the LDS atomics, ~100 cycles per ds_add_f32 wave-instruction, is per instruction).  Here
+// all lanes of a smooth-flow wave take one path: (2r+3) (2r+4) add instructions per wave instead of
+// up to (2r+2) (2r+3) + 2 (2r+2)^2.  Lanes outside the merge condition still add per pixel.
+// grid (pixels/512, C, B).
+template <int R, int WIN>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_patch_backward_gm_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                                    float* __restrict__ gf1, float* __restrict__ gf2) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, PX = 2, MW = K + 2;
+    __shared__ float win[WIN];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * PX;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p0 < n;               // n % 4 == 0: a lane's PX pixels are all valid or all not
+    float fx[PX], fy[PX];
+    int xs[PX], ys[PX];
+    int ymin = 1 << 30;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        fx[k] = fy[k] = 0.f;
+        xs[k] = 0;
+        ys[k] = 1 << 30;
+        if (pv) {
+            float cx = coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale;
+            float cy = coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale;
+            cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
+            cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
+            const float fx0 = floorf(cx), fy0 = floorf(cy);
+            fx[k] = cx - fx0;
+            fy[k] = cy - fy0;
+            xs[k] = (int)fx0 - R;
+            ys[k] = (int)fy0 - R;
+            ymin = min(ymin, max(ys[k], 0));
+        }
+    }
+    // joint box origin and per-pixel offsets inside it
+    const int oy = min(ys[0], ys[1]), ox = min(xs[0], xs[1]);
+    const int dy0 = ys[0] - oy, dy1 = ys[1] - oy, dx0 = xs[0] - ox, dx1 = xs[1] - ox;
+    const bool gm = pv && dy0 + dy1 <= 1 && dx0 + dx1 <= 2;      // |dy| <= 1, |dx| <= 2
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    if (pv) atomicMin(&wmin, ymin);
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    typedef typename FVec<PX>::T v2;
+    auto add = [&](int yy, int xx, float v) {        // LDS window or (rows past it) global
+        if (yy - wy0 < wrows) atomicAdd(win + (yy - wy0) * P.wl + xx, v);
+        else atomicAdd(g2c + (size_t)yy * P.wl + xx, v);
+    };
+    if (pv) {
+        const char* gb = reinterpret_cast<const char*>(g + (size_t)b * D * D * dstride);
+        const unsigned lo1 = (unsigned)(((size_t)c * n + p0) * sizeof(float));
+        const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
+        v2 s1 = v2(0.f);
+        float qprev[PX][K], vprev[PX][K];
+#pragma unroll
+        for (int k = 0; k < PX; ++k)
+#pragma unroll
+            for (int i = 0; i < K; ++i) qprev[k][i] = vprev[k][i] = 0.f;
+#pragma unroll 1
+        for (int j = 0; j <= K; ++j) {     // patch rows 0..K-1, plus the joint box's extra row K
+            float qcur[PX][K];
+            if (j < D) {
+                v2 gr[D];
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    const char* gd = gb + (size_t)(a * D + j) * dstride * sizeof(float);
+                    s1 += *reinterpret_cast<const v2*>(gd + lo1);
+                    gr[a] = *reinterpret_cast<const v2*>(gd + lo2);
+                }
+#pragma unroll
+                for (int k = 0; k < PX; ++k)
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        qcur[k][i] = (i < D ? gr[i][k] * (1.0f - fx[k]) : 0.f) + (i >= 1 ? gr[i - 1][k] * fx[k] : 0.f);
+            } else {
+#pragma unroll
+                for (int k = 0; k < PX; ++k)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) qcur[k][i] = 0.f;
+            }
+            float val[PX][K];              // patch row j of each pixel (0 for j == K)
+#pragma unroll
+            for (int k = 0; k < PX; ++k)
+#pragma unroll
+                for (int i = 0; i < K; ++i) val[k][i] = qcur[k][i] * (1.0f - fy[k]) + qprev[k][i] * fy[k];
+            if (gm) {
+                // joint row j: pixel k contributes its patch row j - dy_k (this row or the previous one)
+                const int yy = oy + j;
+                if (yy >= 0 && yy < P.hl) {
+#pragma unroll
+                    for (int t = 0; t < MW; ++t) {
+                        float m = 0.f;
+#pragma unroll
+                        for (int k = 0; k < PX; ++k) {
+                            const int dyk = k ? dy1 : dy0, dxk = k ? dx1 : dx0;
+                            const float* row = dyk ? vprev[k] : val[k];
+                            // element t - dx_k of the row, dx_k in {0, 1, 2}
+                            const float e0 = t < K ? row[t] : 0.f;
+                            const float e1 = (t >= 1 && t - 1 < K) ? row[t - 1] : 0.f;
+                            const float e2 = (t >= 2 && t - 2 < K) ? row[t - 2] : 0.f;
+                            m += dxk == 0 ? e0 : (dxk == 1 ? e1 : e2);
+                        }
+                        const int xx = ox + t;
+                        if (xx >= 0 && xx < P.wl && m != 0.f) add(yy, xx, m);
+                    }
+                }
+            } else if (j < K) {
+#pragma unroll
+                for (int k = 0; k < PX; ++k) {
+                    const int yy = ys[k] + j;
+                    if (yy < 0 || yy >= P.hl) continue;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xs[k] + i;
+                        if (xx >= 0 && xx < P.wl) add(yy, xx, val[k][i]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < PX; ++k)
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    qprev[k][i] = qcur[k][i];
+                    vprev[k][i] = val[k][i];
+                }
+        }
+        *reinterpret_cast<v2*>(gf1 + ((size_t)b * C + c) * n + p0) = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
+    }
+}
+
 // backward of the general (scaled-grid) stack, raft_dicl_ml levels > 0: every displacement has its
 // own bilinear weights, so each lane (pixel p, channel c) walks the (2r+1)^2 displacements, adds its
 // f1-half gradients into grad_f1 (plain store) and its 4 f2 taps into the workgroup's LDS window
@@ -1610,9 +1759,15 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
             const bool small4 = rows4 * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
             dim3 grid4((height * width / px + kThreads - 1) / kThreads, channels, batch);
             const bool chain = env_variant("RMD_DICL_BWD_CHAIN") != 1;     // 1: no cross-lane run merge (A/B)
+            // product: general two-pixel merge (0.65 vs 0.76 ms smooth flow, 0.79 vs 0.97 ms steep flow at
+            // cfg4, profiles/dicl_bwd_ab_r02.json); RMD_DICL_BWD_GM=2 (diagnostic) selects backward4
+            const bool gmerge = env_variant("RMD_DICL_BWD_GM") != 2 && env_variant("RMD_DICL_BWD_PX") != 4 &&
+                                env_variant("RMD_DICL_BWD_CHAIN") != 1 && env_variant("RMD_DICL_BWD_WIN") != 1;
             switch (radius) {
 #define RMD_CASE(RR) case RR: \
-                if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                if (gmerge && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (gmerge) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (small4 && chain) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
