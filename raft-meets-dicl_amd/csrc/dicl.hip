@@ -684,9 +684,12 @@ dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __re
 // a wave executes every path one of its lanes takes, a wave with both kinds paid for both (the
 // cost of the LDS atomics, ~100 cycles per ds_add_f32 wave-instruction, is per instruction).  Here
 // all lanes of a smooth-flow wave take one path: (2r+3) (2r+4) add instructions per wave instead of
-// up to (2r+2) (2r+3) + 2 (2r+2)^2.  Lanes outside the merge condition still add per pixel.
+// up to (2r+2) (2r+3) + 2 (2r+2)^2.  Lanes outside the merge condition still add per pixel.  With CH,
+// lanes whose joint box continues the previous lane's two columns further on the same rows (smooth
+// flow) sum the overlapping runs through DPP lane shifts, so only a chain's last lane adds more than
+// its own two new columns (far fewer active lanes per add instruction).
 // grid (pixels/512, C, B).
-template <int R, int WIN>
+template <int R, int WIN, bool CH>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_patch_backward_gm_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                     float* __restrict__ gf1, float* __restrict__ gf2) {
@@ -722,6 +725,17 @@ dicl_stack_patch_backward_gm_kernel(const float* __restrict__ g, const float* __
     const int oy = min(ys[0], ys[1]), ox = min(xs[0], xs[1]);
     const int dy0 = ys[0] - oy, dy1 = ys[1] - oy, dx0 = xs[0] - ox, dx1 = xs[1] - ox;
     const bool gm = pv && dy0 + dy1 <= 1 && dx0 + dx1 <= 2;      // |dy| <= 1, |dx| <= 2
+    // CH: lane l's joint box continues lane l-1's two columns further on the same rows (smooth flow)
+    // -> the wave sums the overlapping runs with DPP lane shifts and each lane adds only its own two
+    // new columns (a chain's last lane adds its whole tail)
+    bool link = false, link_next = false;
+    if constexpr (CH) {
+        const int poy = __builtin_amdgcn_update_dpp((int)0x80000000, oy, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const int pox = __builtin_amdgcn_update_dpp((int)0x80000000, ox, 0x138, 0xf, 0xf, false);
+        const int pgm = __builtin_amdgcn_update_dpp(0, (int)gm, 0x138, 0xf, 0xf, false);
+        link = gm && pgm != 0 && poy == oy && pox + PX == ox;
+        link_next = __builtin_amdgcn_update_dpp(0, (int)link, 0x130, 0xf, 0xf, false) != 0;      // wave_shl:1
+    }
     if (threadIdx.x == 0) wmin = 1 << 30;
     for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
     __syncthreads();
@@ -778,6 +792,7 @@ dicl_stack_patch_backward_gm_kernel(const float* __restrict__ g, const float* __
                 // joint row j: pixel k contributes its patch row j - dy_k (this row or the previous one)
                 const int yy = oy + j;
                 if (yy >= 0 && yy < P.hl) {
+                    float mm[MW];
 #pragma unroll
                     for (int t = 0; t < MW; ++t) {
                         float m = 0.f;
@@ -791,8 +806,26 @@ dicl_stack_patch_backward_gm_kernel(const float* __restrict__ g, const float* __
                             const float e2 = (t >= 2 && t - 2 < K) ? row[t - 2] : 0.f;
                             m += dxk == 0 ? e0 : (dxk == 1 ? e1 : e2);
                         }
+                        mm[t] = m;
+                    }
+                    if constexpr (CH) {
+                        // r_t(l) = mm_l[t] + link_l r_{t+2}(l-1): column ox_l + t of the chain
+#pragma unroll
+                        for (int t = 0; t < MW; ++t) {
+                            const int kmax = (MW - 1 - t) / PX;
+                            float rr = mm[t + PX * kmax];
+#pragma unroll
+                            for (int k = kmax - 1; k >= 0; --k) {
+                                const float up = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rr), 0x138, 0xf, 0xf, false));
+                                rr = mm[t + PX * k] + (link ? up : 0.f);
+                            }
+                            mm[t] = (t < PX || !link_next) ? rr : 0.f;
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < MW; ++t) {
                         const int xx = ox + t;
-                        if (xx >= 0 && xx < P.wl && m != 0.f) add(yy, xx, m);
+                        if (xx >= 0 && xx < P.wl && mm[t] != 0.f) add(yy, xx, mm[t]);
                     }
                 }
             } else if (j < K) {
@@ -1759,14 +1792,18 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
             const bool small4 = rows4 * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
             dim3 grid4((height * width / px + kThreads - 1) / kThreads, channels, batch);
             const bool chain = env_variant("RMD_DICL_BWD_CHAIN") != 1;     // 1: no cross-lane run merge (A/B)
-            // product: general two-pixel merge (0.65 vs 0.76 ms smooth flow, 0.79 vs 0.97 ms steep flow at
-            // cfg4, profiles/dicl_bwd_ab_r02.json); RMD_DICL_BWD_GM=2 (diagnostic) selects backward4
+            // product: general two-pixel merge + cross-lane chain (0.55 vs 0.75 ms smooth flow, 0.77 vs 0.96
+            // ms steep flow at cfg4, profiles/dicl_bwd_ab_r02.json); diagnostic RMD_DICL_BWD_GM: 2 selects
+            // backward4, 1 the merge without the chain
             const bool gmerge = env_variant("RMD_DICL_BWD_GM") != 2 && env_variant("RMD_DICL_BWD_PX") != 4 &&
                                 env_variant("RMD_DICL_BWD_CHAIN") != 1 && env_variant("RMD_DICL_BWD_WIN") != 1;
+            const bool gchain = env_variant("RMD_DICL_BWD_GM") != 1;       // 1 (diagnostic): merge without the chain
             switch (radius) {
 #define RMD_CASE(RR) case RR: \
-                if (gmerge && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (gmerge) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                if (gmerge && gchain && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (gmerge && gchain) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (gmerge && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else if (gmerge) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 else if (small4 && chain) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""A/B of the unit-step DICL stack backward kernels (diagnostic build; RMD_DICL_BWD_GM=2: backward4,
-the one-column merge + cross-lane chain; 0 / default: the product's general two-pixel merge) at cfg4 1/8 (B8 C32
-48x160 r4) with smooth coordinates (bench_components.smooth_coords) and with a steeper flow field.
-Gradients of each variant are compared with the first's; times are medians of HIP-event-timed
-forward+backward minus forward.  usage: python tools/dicl_bwd_ab.py [reps] -> JSON"""
+"""A/B of the unit-step DICL stack backward kernels (diagnostic build; RMD_DICL_BWD_GM=2: backward4, the
+one-column merge + cross-lane chain; 1: the general two-pixel merge without a chain; 0 / default: the
+product, general merge + cross-lane chain) at cfg4 1/8 (B8 C32 48x160 r4) with smooth coordinates
+(bench_components.smooth_coords) and with a steeper flow field.  Gradients of each variant are
+compared with the first's; times are medians of HIP-event-timed forward+backward minus forward.
+usage: python tools/dicl_bwd_ab.py [reps] -> JSON"""
 import json
 import os
 import sys
@@ -45,7 +46,7 @@ def main():
         gst = torch.randn(b, 9, 9, 2 * c, h, w, generator=g).to(dev)
         out = {}
         ref = None
-        for v in ("2", "0"):
+        for v in ("2", "1", "0"):
             os.environ["RMD_DICL_BWD_GM"] = v
 
             def fb():
