@@ -1043,6 +1043,193 @@ dicl_stack_sep_backward_kernel(const float* __restrict__ g, const float* __restr
     }
 }
 
+// Separable backward, two pixels per lane with the unit-step kernel's merge: when both pixels' K x K
+// patches fit and their origins differ by <= 1 row and <= 2 columns (any smooth flow; at level-1
+// scale adjacent pixels' origins move half a column), the patches are summed in registers over their
+// joint (K+1) x (K+2) box and, where lane l's box sits one column right of lane l-1's on the same rows
+// (the common step: 2 pixels x 0.5), the overlapping runs are summed through DPP lane shifts so each
+// lane adds only its one new column (a chain's last lane its whole tail).  Other lanes add per pixel
+// (or per tap).  grid (pixels / 512, C, B).
+template <int K, int WIN>
+__global__ void __launch_bounds__(kThreads)
+dicl_stack_sep_backward2_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
+                                float* __restrict__ gf1, float* __restrict__ gf2) {
+    constexpr int PX = 2, MW = K + 2, MH = K + 1;
+    __shared__ float win[WIN];
+    __shared__ int wmin;
+    const int n = P.h * P.w, nl = P.hl * P.wl;
+    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * PX;
+    const int c = blockIdx.y, b = blockIdx.z;
+    const bool pv = p0 < n;                       // n % 4 == 0: both pixels valid or neither
+    const int d = 2 * P.radius + 1;
+    float cxs[PX], cys[PX];
+    int xbase[PX], ybase[PX];
+    bool fits[PX];
+    int ymin = 1 << 30;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+        cxs[k] = cys[k] = 0.f;
+        if (pv) {
+            cxs[k] = fminf(fmaxf(coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale, -1.0e6f), 1.0e6f);
+            cys[k] = fminf(fmaxf(coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale, -1.0e6f), 1.0e6f);
+        }
+        ybase[k] = (int)floorf((cys[k] - (float)P.radius) * P.sy);
+        xbase[k] = (int)floorf((cxs[k] - (float)P.radius) * P.sx);
+        const float pxl = (cxs[k] + (float)P.radius) * P.sx, pyl = (cys[k] + (float)P.radius) * P.sy;
+        fits[k] = (int)floorf(pxl) - xbase[k] <= K - 2 && (int)floorf(pyl) - ybase[k] <= K - 2;
+        if (pv) ymin = min(ymin, max(ybase[k], 0));
+    }
+    const int oy = min(ybase[0], ybase[1]), ox = min(xbase[0], xbase[1]);
+    const int dy0 = ybase[0] - oy, dy1 = ybase[1] - oy, dx0 = xbase[0] - ox, dx1 = xbase[1] - ox;
+    const bool gm = pv && fits[0] && fits[1] && dy0 + dy1 <= 1 && dx0 + dx1 <= 2;
+    const int pys = __builtin_amdgcn_update_dpp((int)0x80000000, oy, 0x138, 0xf, 0xf, false);   // wave_shr:1
+    const int pxs = __builtin_amdgcn_update_dpp((int)0x80000000, ox, 0x138, 0xf, 0xf, false);
+    const int pgm = __builtin_amdgcn_update_dpp(0, (int)gm, 0x138, 0xf, 0xf, false);
+    const bool link = gm && pgm != 0 && pys == oy && pxs + 1 == ox;
+    const bool link_next = __builtin_amdgcn_update_dpp(0, (int)link, 0x130, 0xf, 0xf, false) != 0;   // wave_shl:1
+    if (threadIdx.x == 0) wmin = 1 << 30;
+    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
+    __syncthreads();
+    if (pv) atomicMin(&wmin, ymin);
+    __syncthreads();
+    const int wy0 = min(wmin, P.hl);
+    const int wrows = min(P.hl - wy0, WIN / P.wl);
+    const int C = P.C, C2 = 2 * C + P.extra;
+    const size_t dstride = (size_t)C2 * n;
+    float* g2c = gf2 + ((size_t)b * C + c) * nl;
+    auto add = [&](int yy, int xx, float v) {            // LDS window or (rows past it) global
+        if (yy >= wy0 && yy - wy0 < wrows) atomicAdd(win + (yy - wy0) * P.wl + xx, v);
+        else atomicAdd(g2c + (size_t)yy * P.wl + xx, v);
+    };
+    typedef typename FVec<PX>::T v2;
+    if (pv) {
+        const char* gb = reinterpret_cast<const char*>(g + (size_t)b * d * d * dstride);
+        const unsigned lo1 = (unsigned)(((size_t)c * n + p0) * sizeof(float));
+        const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
+        v2 s1 = v2(0.f);
+        float patch[PX][K][K];
+#pragma unroll
+        for (int k = 0; k < PX; ++k)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) patch[k][j][i] = 0.f;
+        const bool any_fit = fits[0] || fits[1];
+        for (int bb = 0; bb < d; ++bb) {
+            float row[PX][K];
+#pragma unroll
+            for (int k = 0; k < PX; ++k)
+#pragma unroll
+                for (int i = 0; i < K; ++i) row[k][i] = 0.f;
+            for (int a = 0; a < d; ++a) {
+                const char* gd = gb + (size_t)(a * d + bb) * dstride * sizeof(float);
+                s1 += *reinterpret_cast<const v2*>(gd + lo1);
+                const v2 gv = *reinterpret_cast<const v2*>(gd + lo2);
+#pragma unroll
+                for (int k = 0; k < PX; ++k) {
+                    if (fits[k]) {
+                        const float px = (cxs[k] + (float)(a - P.radius)) * P.sx;
+                        const float fx0 = floorf(px);
+                        const int rx = (int)fx0 - xbase[k];
+                        const float w1 = (px - fx0) * gv[k], w0 = gv[k] - w1;
+#pragma unroll
+                        for (int i = 0; i < K; ++i) row[k][i] += i == rx ? w0 : (i == rx + 1 ? w1 : 0.f);
+                    } else {                           // per-tap path (fp32 rounding at a span bound)
+                        const Taps t = make_taps((cxs[k] + (float)(a - P.radius)) * P.sx,
+                                                 (cys[k] + (float)(bb - P.radius)) * P.sy, P.hl, P.wl);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (t.wgt[q] != 0.f) add(t.idx[q] / P.wl, t.idx[q] % P.wl, gv[k] * t.wgt[q]);
+                    }
+                }
+            }
+            if (any_fit) {
+#pragma unroll
+                for (int k = 0; k < PX; ++k) {
+                    const float py = (cys[k] + (float)(bb - P.radius)) * P.sy;
+                    const float fy0 = floorf(py);
+                    const int ry = (int)fy0 - ybase[k];
+                    const float fy = py - fy0;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        const float wy = j == ry ? 1.f - fy : (j == ry + 1 ? fy : 0.f);
+#pragma unroll
+                        for (int i = 0; i < K; ++i) patch[k][j][i] = fmaf(wy, row[k][i], patch[k][j][i]);
+                    }
+                }
+            }
+        }
+        if (gm) {
+#pragma unroll
+            for (int r = 0; r < MH; ++r) {
+                const int yy = oy + r;
+                if (yy < 0 || yy >= P.hl) continue;
+                float mm[MW];
+#pragma unroll
+                for (int t = 0; t < MW; ++t) {
+                    float m = 0.f;
+#pragma unroll
+                    for (int k = 0; k < PX; ++k) {
+                        // element (r - dy_k, t - dx_k) of pixel k's patch: select among the compile-time
+                        // candidates rows {r, r-1} x columns {t, t-1, t-2}
+                        const int dyk = k ? dy1 : dy0, dxk = k ? dx1 : dx0;
+                        float e[3];
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) {
+                            const int i = t - q;
+                            const float a0 = (i >= 0 && i < K && r < K) ? patch[k][r < K ? r : 0][i >= 0 && i < K ? i : 0] : 0.f;
+                            const float a1 = (i >= 0 && i < K && r >= 1 && r - 1 < K)
+                                                 ? patch[k][r >= 1 && r - 1 < K ? r - 1 : 0][i >= 0 && i < K ? i : 0] : 0.f;
+                            e[q] = dyk ? a1 : a0;
+                        }
+                        m += dxk == 0 ? e[0] : (dxk == 1 ? e[1] : e[2]);
+                    }
+                    mm[t] = m;
+                }
+                // r_t(l) = mm_l[t] + link_l r_{t+1}(l-1): column ox_l + t of the chain
+#pragma unroll
+                for (int t = 0; t < MW; ++t) {
+                    const int kmax = MW - 1 - t;
+                    float rr = mm[t + kmax];
+#pragma unroll
+                    for (int q = kmax - 1; q >= 0; --q) {
+                        const float up = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rr), 0x138, 0xf, 0xf, false));
+                        rr = mm[t + q] + (link ? up : 0.f);
+                    }
+                    mm[t] = (t < 1 || !link_next) ? rr : 0.f;
+                }
+#pragma unroll
+                for (int t = 0; t < MW; ++t) {
+                    const int xx = ox + t;
+                    if (xx >= 0 && xx < P.wl && mm[t] != 0.f) add(yy, xx, mm[t]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PX; ++k) {
+                if (!fits[k]) continue;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const int yy = ybase[k] + j;
+                    if (yy < 0 || yy >= P.hl) continue;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const int xx = xbase[k] + i;
+                        if (xx >= 0 && xx < P.wl && patch[k][j][i] != 0.f) add(yy, xx, patch[k][j][i]);
+                    }
+                }
+            }
+        }
+        *reinterpret_cast<v2*>(gf1 + ((size_t)b * C + c) * n + p0) = s1;
+    }
+    __syncthreads();
+    float* gw = g2c + (size_t)wy0 * P.wl;
+    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
+        const float v = win[k];
+        if (v != 0.f) atomicAdd(gw + k, v);
+    }
+}
+
 // ---- DICL baseline integer volume ------------------------------------------------------------
 struct IntParams {
     int B, C, h, w, ru, rv;
@@ -1843,6 +2030,22 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
         const float span = 2.0f * radius * std::max(P.sx, P.sy);
         const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
+        // two pixels per lane with the merged / chained patch adds (K <= 8); RMD_DICL_BWD_SEP2=2
+        // (diagnostic) selects the one-pixel kernel
+        if (k <= 8 && env_variant("RMD_DICL_BWD_SEP2") != 2) {
+            const float rows2 = 2.0f * radius * std::max(P.sy, 1.0f) + 512.0f / width * std::max(P.sy, 0.5f) + 10.0f;
+            const bool small2 = rows2 * level_width <= (float)kWinSmall;
+            dim3 grid2((height * width / 2 + kThreads - 1) / kThreads, channels, batch);
+            switch (k) {
+#define RMD_KCASE2(KK) case KK: \
+                if (small2) dicl_stack_sep_backward2_kernel<KK, kWinSmall><<<grid2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else dicl_stack_sep_backward2_kernel<KK, kWinFloats><<<grid2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                return check_launch("rmd_dicl_stack_backward/separable2");
+                RMD_KCASE2(4) RMD_KCASE2(6) RMD_KCASE2(8)
+#undef RMD_KCASE2
+                default: break;
+            }
+        }
         switch (k) {
 #define RMD_KCASE(KK) case KK: \
             if (small_win) dicl_stack_sep_backward_kernel<KK, kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \

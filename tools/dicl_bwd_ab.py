@@ -60,6 +60,24 @@ def main():
             out[v]["bwd_ms"] = out[v]["fwd_bwd_ms"] - fwd
         os.environ.pop("RMD_DICL_BWD_GM", None)
         res[name] = out
+        # raft_dicl_ml level 1 (fmap2 at 24x80, separable kernels): RMD_DICL_BWD_SEP2=2 one pixel per
+        # lane, 0 / default two pixels per lane with merged + chained adds
+        f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev).requires_grad_(True)
+        outl, refl = {}, None
+        for v in ("2", "0"):
+            os.environ["RMD_DICL_BWD_SEP2"] = v
+
+            def fbl():
+                return torch.autograd.grad(ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), (f1, f2l), gst)
+            got = fbl()
+            if refl is None:
+                refl = [t.clone() for t in got]
+            err = max(float((x - y).abs().max() / y.abs().max()) for x, y in zip(got, refl))
+            fwd = med(lambda: ops.dicl_stack(f1.detach(), f2l.detach(), co, r, level=1, norm_hw=(h, w)), reps)
+            outl[v] = {"fwd_bwd_ms": med(fbl, reps), "fwd_ms": fwd, "max_rel_err_vs_first": err}
+            outl[v]["bwd_ms"] = outl[v]["fwd_bwd_ms"] - fwd
+        os.environ.pop("RMD_DICL_BWD_SEP2", None)
+        res[name + "_ml_level1"] = outl
     print(json.dumps(res, indent=1))
 
 
