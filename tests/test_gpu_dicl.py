@@ -257,3 +257,30 @@ def test_dicl_stack_backward_smooth_flow_vs_oracle(radius):
     r1, r2 = oracle.dicl_stack_backward(f2.shape, co.astype(np.float64), radius, gst.astype(np.float64))
     assert rel_max_err(g1.cpu().numpy(), r1) < 1e-5
     assert rel_max_err(g2.cpu().numpy(), r2) < 1e-4
+
+
+@pytest.mark.parametrize("level,radius,amp", [(0, 4, 3.0), (0, 4, 8.0), (0, 3, 3.0), (0, 1, 8.0), (1, 4, 3.0),
+                                              (1, 4, 8.0), (1, 3, 3.0)])
+def test_dicl_stack_backward_graded_flow_vs_oracle(level, radius, amp):
+    """Stack backward under flow fields with gradients (low-resolution noise upsampled x8, as the
+    component bench): neighbouring pixels' window origins step by 0, 1 or 2 columns and change rows
+    along x, so the two-pixel merges (unit step: joint (2r+3) x (2r+4) box; level 1: K x K separable
+    patches) mix with chained, unchained and per-pixel lanes inside one wave."""
+    import rmd
+    rng = np.random.default_rng(int(100 * amp) + 10 * level + radius)
+    b, c, h, w = 2, 8, 24, 96
+    hl, wl = h >> level, w >> level
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, hl, wl)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    low = torch.from_numpy(rng.standard_normal((b, 2, h // 8, w // 8)) * amp)
+    flow = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=True).numpy()
+    co = (np.stack([xs, ys])[None] + flow).astype(np.float32)
+    t1, t2 = _t(f1, True), _t(f2, True)
+    st = rmd.ops.dicl_stack(t1, t2, _t(co), radius, level=level, norm_hw=(h, w))
+    gst = rng.standard_normal(tuple(st.shape)).astype(np.float32)
+    g1, g2 = torch.autograd.grad(st, (t1, t2), _t(gst))
+    r1, r2 = oracle.dicl_stack_backward(f2.shape, co.astype(np.float64), radius, gst.astype(np.float64),
+                                        level=level, norm_hw=(h, w))
+    assert rel_max_err(g1.cpu().numpy(), r1) < 1e-5
+    assert rel_max_err(g2.cpu().numpy(), r2) < 1e-4
