@@ -12,6 +12,11 @@
 //   f32   16x16x4 : lane (g, i) holds channels 16*ls + 4*m + g, m < 4           (four MFMAs per step)
 // so operand loads are whole 128-B lines (the row-per-lane gather of a pixel-major layout touches 32
 // lines per instruction and halves the L1 rate).  Query rows (fmap1 * scale) use the same layout.
+// fp32 mode (X3) stores every value as a split bf16 pair v = hi + lo (hi = bf16(v), lo = bf16(v - hi)):
+// each bf16 load step is followed by its lo step, and a task accumulates lo.hi + hi.lo + hi.hi with the
+// 16x16x32 bf16 MFMA (the dropped lo.lo term is ~2^-16 relative; same split as the fp32-mode GEMM).
+// Same workspace bytes as f32 operands; the exact f32 MFMA form stays in the diagnostic build
+// (RMD_OTF_EXACT=1).
 //
 // Lookup: one 256-thread block per (16 x 2 query block, batch), looping over the levels.  The 32 queries' (2r+2)^2
 // integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
@@ -133,9 +138,10 @@ struct LevelSrc {
 // Segment operands: one thread per 16-B lane chunk (segment, load step, lane); a wave writes one
 // contiguous 1-KiB load step, its reads run along x within each channel.
 // levels = 1 and scale = s give the query operand (fmap1 * s).
-template <typename T>
+template <typename T, bool X3>
 __global__ void __launch_bounds__(kThreads)
 otf_segments_kernel(LevelSrc src, OtfGeom g, float scale, T* __restrict__ seg) {
+    static_assert(!X3 || sizeof(T) == 2, "split pairs are bf16");
     using S = Seg<T>;
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
     const int nls = g.Cp / S::LSC;
@@ -156,28 +162,53 @@ otf_segments_kernel(LevelSrc src, OtfGeom g, float scale, T* __restrict__ seg) {
     const size_t plane = (size_t)g.lh[l] * g.lw[l];
     const float* base = src.p[l] + (size_t)b * g.C * plane + (size_t)y * g.lw[l] + x;
     typedef __attribute__((ext_vector_type(S::LE))) T frag_t;
-    frag_t v;
+    frag_t v, vl;
 #pragma unroll
     for (int e = 0; e < S::LE; ++e) {
         // channel of element e of lane group gq (inverse of Seg::lane_g / Seg::elem)
         const int c = S::LE == 8 ? ls * 32 + gq * 8 + e : ls * 16 + 4 * e + gq;
-        v[e] = (T)(x < g.lw[l] && c < g.C ? base[(size_t)c * plane] * scale : 0.f);
+        const float f = x < g.lw[l] && c < g.C ? base[(size_t)c * plane] * scale : 0.f;
+        v[e] = (T)f;
+        if constexpr (X3) vl[e] = (T)(f - (float)v[e]);
     }
-    *reinterpret_cast<frag_t*>(seg + (size_t)idx * S::LE) = v;
+    if constexpr (X3) {
+        // load step (r, hi) then (r, lo): r = idx >> 6 counts (segment, step) pairs
+        T* o = seg + ((size_t)(idx >> 6) * 128 + lane) * S::LE;
+        *reinterpret_cast<frag_t*>(o) = v;
+        *reinterpret_cast<frag_t*>(o + 64 * S::LE) = vl;
+    } else {
+        (void)vl;
+        *reinterpret_cast<frag_t*>(seg + (size_t)idx * S::LE) = v;
+    }
 }
 
-// element (pixel i of segment, channel c) of a segment operand
-template <typename T>
+// element (pixel i of segment, channel c) of a segment operand (X3: hi + lo)
+template <typename T, bool X3>
 __device__ __forceinline__ float seg_elem(const T* segbase, int i, int c) {
     using S = Seg<T>;
-    return (float)segbase[(c / S::LSC) * 64 * S::LE + (S::lane_g(c) * 16 + i) * S::LE + S::elem(c)];
+    constexpr int NP = X3 ? 2 : 1;
+    const T* p = segbase + (c / S::LSC) * NP * 64 * S::LE + (S::lane_g(c) * 16 + i) * S::LE + S::elem(c);
+    if constexpr (X3) return (float)p[0] + (float)p[64 * S::LE];
+    return (float)p[0];
+}
+
+// one 16x16 tile's products of one load step: t / q point at the step's fragment(s)
+template <typename T, bool X3>
+__device__ __forceinline__ void seg_mma(f32x4& acc, const typename Seg<T>::frag* t, const typename Seg<T>::frag* q) {
+    if constexpr (X3) {
+        Seg<T>::mma(acc, t[1], q[0]);        // lo.hi, hi.lo first, hi.hi last
+        Seg<T>::mma(acc, t[0], q[1]);
+        Seg<T>::mma(acc, t[0], q[0]);
+    } else {
+        Seg<T>::mma(acc, t[0], q[0]);
+    }
 }
 
 // 1-D grid over (batch, query block), XCD-aware: adjacent query blocks, whose target boxes overlap,
 // run on the same XCD and share its L2.  One block runs every level of its 32 queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, int R, int CPT, bool PF>
+template <typename T, bool X3, int R, int CPT, bool PF>
 __global__ void __launch_bounds__(kLookThreads, PF ? 2 : 1)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out, int ablate) {
@@ -198,16 +229,17 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     const int qx0 = (qb % nbx) * kBX, qy0 = (qb / nbx) * kBY;
     const int N = g.H * g.W;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NP = X3 ? 2 : 1;                      // load steps per channel step (X3: hi, lo)
     const int cp = CPT > 0 ? CPT : g.Cp;
     const int nls = cp / SG::LSC;
-    const size_t segsz = (size_t)16 * cp;
+    const size_t segsz = (size_t)16 * cp * NP;
     const T* qsb = qseg + ((size_t)b * g.QS + (size_t)qy0 * g.qnsx + (qx0 >> 4)) * segsz;
     const T* qsb1 = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + 1, g.H - 1) * g.qnsx + (qx0 >> 4)) * segsz;
 
     // the block's two query segments (CPT > 0): one coalesced copy into LDS, overlapping the coords
     // load; each wave then keeps its register fragments for every level and target segment
-    constexpr int NLS = CPT > 0 ? CPT / SG::LSC : 1;
-    constexpr int QV = CPT > 0 ? 16 * CPT * (int)sizeof(T) / 16 : 0;     // 16-B vectors per segment
+    constexpr int NLS = CPT > 0 ? CPT / SG::LSC * NP : 1;                 // load steps per segment
+    constexpr int QV = CPT > 0 ? 16 * CPT * NP * (int)sizeof(T) / 16 : 0;     // 16-B vectors per segment
     static_assert(2 * QV * 16 <= kQ * kLd * 4, "two query segments must fit the S buffer");
     if constexpr (CPT > 0) {
         const uint4* s0 = reinterpret_cast<const uint4*>(qsb);
@@ -318,9 +350,9 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                         else if (task + kWaves < ntask) tload(tn, task + kWaves);
                         f32x4 a0 = {}, a1 = {};
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ++ls) {
-                            SG::mma(a0, tc[ls], q0[ls]);
-                            SG::mma(a1, tc[ls], q1[ls]);
+                        for (int ls = 0; ls < NLS; ls += NP) {
+                            seg_mma<T, X3>(a0, tc + ls, q0 + ls);
+                            seg_mma<T, X3>(a1, tc + ls, q1 + ls);
                         }
                         store(a0, a1, task);
                         if (PF) {
@@ -332,12 +364,16 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     for (int task = w; task < ntask; task += kWaves) {
                         const T* tsb = tptr(task);
                         f32x4 a0 = {}, a1 = {};
-                        for (int ls = 0; ls < nls; ++ls) {
-                            const frag t = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-                            const frag u0 = *reinterpret_cast<const frag*>(qsb + ((size_t)ls * 64 + lane) * SG::LE);
-                            const frag u1 = *reinterpret_cast<const frag*>(qsb1 + ((size_t)ls * 64 + lane) * SG::LE);
-                            SG::mma(a0, t, u0);
-                            SG::mma(a1, t, u1);
+                        for (int ls = 0; ls < nls * NP; ls += NP) {
+                            frag t[NP], u0[NP], u1[NP];
+#pragma unroll
+                            for (int p = 0; p < NP; ++p) {
+                                t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
+                                u0[p] = *reinterpret_cast<const frag*>(qsb + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                                u1[p] = *reinterpret_cast<const frag*>(qsb1 + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                            }
+                            seg_mma<T, X3>(a0, t, u0);
+                            seg_mma<T, X3>(a1, t, u1);
                         }
                         store(a0, a1, task);
                     }
@@ -376,7 +412,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
                     const T* qs = q < kBX ? qsb : qsb1;
                     const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
-                    for (int c = 0; c < g.C; ++c) acc = fmaf(seg_elem(qs, q % kBX, c), seg_elem(ts, tx & 15, c), acc);
+                    for (int c = 0; c < g.C; ++c)
+                        acc = fmaf(seg_elem<T, X3>(qs, q % kBX, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
                 }
                 S[q * kLd + r] = acc;
             }
@@ -414,6 +451,13 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     }
 }
 
+// fp32 mode: split-bf16 MFMA (product) or the exact f32 MFMA (diagnostic build, RMD_OTF_EXACT=1); the
+// prepare and the lookup must agree, so the knob is read once per process
+bool otf_exact() {
+    static const bool e = env_knob("RMD_OTF_EXACT", 0) != 0;
+    return e;
+}
+
 int check_otf(int batch, int channels, int height, int width, int levels, int compute) {
     RMD_REQUIRE(batch > 0 && channels > 0 && height > 0 && width > 0, RMD_ERR_SHAPE, "rmd_corr_otf: bad sizes");
     RMD_REQUIRE(levels >= 1 && levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_otf: bad levels");
@@ -423,10 +467,10 @@ int check_otf(int batch, int channels, int height, int width, int levels, int co
     return RMD_OK;
 }
 
-template <typename T>
+template <typename T, bool X3>
 void launch_segments(const LevelSrc& src, const OtfGeom& g, float scale, T* seg, hipStream_t st) {
     const long long n = (long long)g.B * g.TS * (g.Cp / Seg<T>::LSC) * 64;
-    otf_segments_kernel<T><<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, st>>>(src, g, scale, seg);
+    otf_segments_kernel<T, X3><<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, 0, st>>>(src, g, scale, seg);
 }
 
 }  // namespace
@@ -465,12 +509,16 @@ extern "C" int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int 
     const size_t qn = otf_query_elems(g);
     if (compute == RMD_BF16) {
         __bf16* q = reinterpret_cast<__bf16*>(workspace);
-        launch_segments<__bf16>(lq, g1, scale, q, st);
-        launch_segments<__bf16>(lt, g, 1.0f, q + qn, st);
+        launch_segments<__bf16, false>(lq, g1, scale, q, st);
+        launch_segments<__bf16, false>(lt, g, 1.0f, q + qn, st);
+    } else if (!otf_exact()) {
+        __bf16* q = reinterpret_cast<__bf16*>(workspace);          // split pairs: 2 x qn bf16 = qn floats
+        launch_segments<__bf16, true>(lq, g1, scale, q, st);
+        launch_segments<__bf16, true>(lt, g, 1.0f, q + 2 * qn, st);
     } else {
         float* q = reinterpret_cast<float*>(workspace);
-        launch_segments<float>(lq, g1, scale, q, st);
-        launch_segments<float>(lt, g, 1.0f, q + qn, st);
+        launch_segments<float, false>(lq, g1, scale, q, st);
+        launch_segments<float, false>(lt, g, 1.0f, q + qn, st);
     }
     return check_launch("rmd_corr_otf_prepare");
 }
@@ -496,18 +544,20 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     const bool force_rt = env_knob("RMD_OTF_RUNTIME", 0) != 0;
 #ifdef RMD_DIAG
     const bool pf = env_knob("RMD_OTF_PF", 0) != 0;
-#define RMD_OTF_K(T, RR, CC) (pf ? otf_lookup_kernel<T, RR, CC, true> : otf_lookup_kernel<T, RR, CC, false>)
+#define RMD_OTF_K(T, RR, CC) (pf ? otf_lookup_kernel<T, XS, RR, CC, true> : otf_lookup_kernel<T, XS, RR, CC, false>)
 #else
-#define RMD_OTF_K(T, RR, CC) otf_lookup_kernel<T, RR, CC, false>
+#define RMD_OTF_K(T, RR, CC) otf_lookup_kernel<T, XS, RR, CC, false>
 #endif
-    const int cpt = force_rt || (compute == RMD_F32 && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
+    const bool exact = compute == RMD_F32 && otf_exact();
+    const bool x3 = compute == RMD_F32 && !exact;
+    const int cpt = force_rt || (exact && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
 #define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \
         auto k = RMD_OTF_K(T, RR, CC);                                                                         \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
-        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn, g, coords, zero_level_mask, out, ablate);              \
+        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn * XN, g, coords, zero_level_mask, out, ablate);   \
     } while (0)
 #define RMD_OTF_C(T, RR)                                 \
     switch (cpt) {                                       \
@@ -529,8 +579,16 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         default: RMD_OTF_C(T, 8); break;                 \
     }
     if (compute == RMD_BF16) {
+        constexpr bool XS = false;
+        constexpr size_t XN = 1;
+        RMD_OTF_R(__bf16)
+    } else if (x3) {
+        constexpr bool XS = true;
+        constexpr size_t XN = 2;                    // query segments: qn split pairs
         RMD_OTF_R(__bf16)
     } else {
+        constexpr bool XS = false;
+        constexpr size_t XN = 1;
         RMD_OTF_R(float)
     }
 #undef RMD_OTF_R
