@@ -289,6 +289,7 @@ dicl_stack_grad_f2_kernel(const float* __restrict__ g, const float* __restrict__
 template <int PX> struct FVec;
 template <> struct FVec<4> { typedef __attribute__((ext_vector_type(4))) float T; };
 template <> struct FVec<2> { typedef __attribute__((ext_vector_type(2))) float T; };
+template <> struct FVec<1> { typedef __attribute__((ext_vector_type(1))) float T; };
 
 template <bool NT, typename V>
 __device__ __forceinline__ void stv(float* p, V v) {
@@ -302,8 +303,8 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
                         StackParams P, int nxb, int remap, float* __restrict__ out) {
     // PX consecutive pixels per lane (each with its own patch) so every store is a PX-float vector
     // (PX * 256 B per wave-instruction); one channel per thread: 1-D grid of (pixels / 256 PX) x C x B
-    // blocks, remapped so an XCD works on one batch image (its f2 stays in that XCD's L2).  PX = 2
-    // keeps the two interpolated rows of r = 3, 4 in ~100 VGPRs (4 waves per SIMD); PX = 4 needs ~200.
+    // blocks, optionally remapped so an XCD works on one batch image.  Product PX = 1: 56 VGPRs at
+    // r = 4, 7 waves per SIMD, the most stores in flight (PX = 2 needs ~106 VGPRs, PX = 4 ~200).
     typedef typename FVec<PX>::T V;
     constexpr int D = 2 * R + 1, K = 2 * R + 2;
     const int n = P.h * P.w, nl = P.hl * P.wl;
@@ -1902,21 +1903,24 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
     const int d = 2 * radius + 1;
     const double image_bytes = 4.0 * d * d * (2.0 * channels + P.extra) * height * width;
     if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4 && image_bytes < 4294967296.0) {
-        // RMD_DICL_PATCH (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = XCD remap, 3 = 4 pixels per lane.
-        // Measured at cfg4 (profiles/dicl_ab_r01.json): non-temporal stores are the win (0.33 -> 0.26 ms);
-        // the XCD remap does not help (f2 re-reads hit the MALL either way)
+        // RMD_DICL_PATCH (A/B, tools/dicl_ab.py): 1 = plain stores (2 pixels per lane), 2 = XCD remap
+        // (2 pixels), 3 = 4 pixels per lane, 4 = 2 pixels per lane (round-1 product), 5 = 1 pixel + XCD remap.
+        // Measured at cfg4 (profiles/dicl_ab_r01.json, dicl_px_ab_r02.json): non-temporal stores are the
+        // win (0.33 -> 0.26 ms); one pixel per lane (56 VGPRs, 7 waves per SIMD instead of 4) keeps more
+        // stores in flight: 0.238 vs 0.256 ms
         const int var = env_variant("RMD_DICL_PATCH");
-        const int px = var == 3 ? 4 : 2;
+        const int px = var == 3 ? 4 : (var == 0 || var == 5) ? 1 : 2;
         const int nxb = (height * width / px + kThreads - 1) / kThreads;
         const long long nwg = (long long)nxb * channels * batch;
         RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack: grid too large");
-        const int remap = var == 2;
+        const int remap = var == 2 || var == 5;
         hipStream_t st = as_stream(stream);
         switch (radius) {
 #define RMD_CASE(RR) case RR: \
             if (var == 1) dicl_stack_patch_kernel<RR, 2, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
             else if (var == 3) dicl_stack_patch_kernel<RR, 4, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
-            else dicl_stack_patch_kernel<RR, 2, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            else if (var == 2 || var == 4) dicl_stack_patch_kernel<RR, 2, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            else dicl_stack_patch_kernel<RR, 1, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
             break;
             RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE

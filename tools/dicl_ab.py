@@ -3,7 +3,7 @@
 BASELINE shapes: a6 rmd_dicl_stack at cfg4 1/8 (B8 C32 48x160 r4), a7 its raft_dicl_ml level-1 form (f2 at 24x80), a8 rmd_dicl_stack_int at cfg3
 level 2 (B8 C32 96x128 ru=rv=3).  Each variant's output is compared bitwise with variant 1's (the
 previous formulation); times are medians of HIP-event-timed launches, interleaved over rounds.
-usage: python tools/dicl_ab.py [reps] -> one JSON document on stdout"""
+usage: python tools/dicl_ab.py [reps] [name filter] -> one JSON document on stdout"""
 import json
 import os
 import sys
@@ -42,7 +42,7 @@ def main():
     co = (torch.stack([xs, ys]).float()[None] + flow).to(dev)
     nb = b * 81 * 2 * c * h * w * 4 + 2 * f1.numel() * 4 + co.numel() * 4
     out = torch.empty(b, 9, 9, 2 * c, h, w, device=dev)
-    cases.append(("a6_stack_cfg4", "RMD_DICL_PATCH", ["1", "0", "2", "3"], lambda: ops.dicl_stack(f1, f2, co, r), nb))
+    cases.append(("a6_stack_cfg4", "RMD_DICL_PATCH", ["1", "0", "2", "3", "4", "5"], lambda: ops.dicl_stack(f1, f2, co, r), nb))
     f2l = torch.randn(b, c, h // 2, w // 2, generator=g).to(dev)
     cases.append(("a7_ml_level1_cfg4", "RMD_DICL_GENERAL", ["1", "3", "0"],
                   lambda: ops.dicl_stack(f1, f2l, co, r, level=1, norm_hw=(h, w)), nb - f2.numel() * 3))
@@ -62,7 +62,11 @@ def main():
 
     def bwd7():
         return torch.autograd.grad(ops.dicl_stack(f1g, f2lg, co, r, level=1, norm_hw=(h, w)), (f1g, f2lg), gst)
+    only = sys.argv[2] if len(sys.argv) > 2 else ""
+    cases = [cs for cs in cases if only in cs[0]]
     for name, fn in (("a6_backward_cfg4", bwd6), ("a7_backward_cfg4", bwd7)):
+        if only not in name:
+            continue
         out = {}
         os.environ["RMD_DICL_BWD_WIN"] = "1"
         ref = [t.clone() for t in fn()]
