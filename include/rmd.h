@@ -122,8 +122,8 @@ int rmd_corr_lookup(const void* pyramid, const rmd_pyramid_desc* desc, const flo
  * (src/models/impls/raft_fs.py:13-87; scale = 1) and, with levels = 1 and scale = 1/sqrt(C), the
  * window dot of corr/dot.py:25-57.  rmd_corr_otf_prepare writes the pixel-major query rows
  * (fmap1 * scale) and the avg-pooled target rows of every level into `workspace`
- * (rmd_corr_otf_workspace_bytes; compute RMD_F32 = fp32-accurate split-bf16 MFMA, lo.hi + hi.lo + hi.hi
- * over operands stored as (hi, lo) bf16 pairs; RMD_BF16 = bf16 MFMA);
+ * (rmd_corr_otf_workspace_bytes; compute RMD_BF16X3 = fp32-accurate split-bf16 MFMA, lo.hi + hi.lo +
+ * hi.hi over operands stored as (hi, lo) bf16 pairs; RMD_F32 = exact f32 MFMA; RMD_BF16 = bf16 MFMA);
  * rmd_corr_otf_lookup then produces rmd_corr_lookup's output for `coords` from them each iteration.
  */
 size_t rmd_corr_otf_workspace_bytes(int batch, int channels, int height, int width, int levels, int compute);

@@ -12,11 +12,11 @@
 //   f32   16x16x4 : lane (g, i) holds channels 16*ls + 4*m + g, m < 4           (four MFMAs per step)
 // so operand loads are whole 128-B lines (the row-per-lane gather of a pixel-major layout touches 32
 // lines per instruction and halves the L1 rate).  Query rows (fmap1 * scale) use the same layout.
-// fp32 mode (X3) stores every value as a split bf16 pair v = hi + lo (hi = bf16(v), lo = bf16(v - hi)):
-// each bf16 load step is followed by its lo step, and a task accumulates lo.hi + hi.lo + hi.hi with the
-// 16x16x32 bf16 MFMA (the dropped lo.lo term is ~2^-16 relative; same split as the fp32-mode GEMM).
-// Same workspace bytes as f32 operands; the exact f32 MFMA form stays in the diagnostic build
-// (RMD_OTF_EXACT=1).
+// compute RMD_BF16X3 (the fp32 precision mode) stores every value as a split bf16 pair v = hi + lo
+// (hi = bf16(v), lo = bf16(v - hi)): each bf16 load step is followed by its lo step, and a task
+// accumulates lo.hi + hi.lo + hi.hi with the 16x16x32 bf16 MFMA (the dropped lo.lo term is ~2^-16
+// relative; same split as the fp32-mode GEMM), in the workspace bytes of f32 operands.  RMD_F32 keeps
+// the exact f32 MFMA (fp32-exact).
 //
 // Lookup: one 256-thread block per (16 x 2 query block, batch), looping over the levels.  The 32 queries' (2r+2)^2
 // integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
@@ -451,19 +451,13 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     }
 }
 
-// fp32 mode: split-bf16 MFMA (product) or the exact f32 MFMA (diagnostic build, RMD_OTF_EXACT=1); the
-// prepare and the lookup must agree, so the knob is read once per process
-bool otf_exact() {
-    static const bool e = env_knob("RMD_OTF_EXACT", 0) != 0;
-    return e;
-}
-
 int check_otf(int batch, int channels, int height, int width, int levels, int compute) {
     RMD_REQUIRE(batch > 0 && channels > 0 && height > 0 && width > 0, RMD_ERR_SHAPE, "rmd_corr_otf: bad sizes");
     RMD_REQUIRE(levels >= 1 && levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_otf: bad levels");
     RMD_REQUIRE((height >> (levels - 1)) >= 1 && (width >> (levels - 1)) >= 1, RMD_ERR_SHAPE,
                 "rmd_corr_otf: level %d of a %dx%d map is empty", levels - 1, height, width);
-    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16, RMD_ERR_ARG, "rmd_corr_otf: compute must be F32 or BF16");
+    RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16 || compute == RMD_BF16X3, RMD_ERR_ARG,
+                "rmd_corr_otf: compute must be F32, BF16 or BF16X3");
     return RMD_OK;
 }
 
@@ -482,7 +476,7 @@ extern "C" size_t rmd_corr_otf_workspace_bytes(int batch, int channels, int heig
                                                int compute) {
     if (check_otf(batch, channels, height, width, levels, compute)) return 0;
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
-    const size_t es = compute == RMD_F32 ? 4 : 2;
+    const size_t es = compute == RMD_BF16 ? 2 : 4;        // BF16X3: (hi, lo) bf16 pairs
     return otf_scratch_offset(g, es) + otf_scratch_elems(g) * 4;
 }
 
@@ -494,7 +488,7 @@ extern "C" int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int 
     hipStream_t st = as_stream(stream);
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
     const OtfGeom g1 = make_otf_geom(batch, channels, height, width, 1);   // query segments: TS = QS
-    const size_t es = compute == RMD_F32 ? 4 : 2;
+    const size_t es = compute == RMD_BF16 ? 2 : 4;
     LevelSrc lq{}, lt{};
     lq.p[0] = fmap1;
     lt.p[0] = fmap2;
@@ -511,7 +505,7 @@ extern "C" int rmd_corr_otf_prepare(const float* fmap1, const float* fmap2, int 
         __bf16* q = reinterpret_cast<__bf16*>(workspace);
         launch_segments<__bf16, false>(lq, g1, scale, q, st);
         launch_segments<__bf16, false>(lt, g, 1.0f, q + qn, st);
-    } else if (!otf_exact()) {
+    } else if (compute == RMD_BF16X3) {
         __bf16* q = reinterpret_cast<__bf16*>(workspace);          // split pairs: 2 x qn bf16 = qn floats
         launch_segments<__bf16, true>(lq, g1, scale, q, st);
         launch_segments<__bf16, true>(lt, g, 1.0f, q + 2 * qn, st);
@@ -548,8 +542,8 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #else
 #define RMD_OTF_K(T, RR, CC) otf_lookup_kernel<T, XS, RR, CC, false>
 #endif
-    const bool exact = compute == RMD_F32 && otf_exact();
-    const bool x3 = compute == RMD_F32 && !exact;
+    const bool exact = compute == RMD_F32;
+    const bool x3 = compute == RMD_BF16X3;
     const int cpt = force_rt || (exact && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
 #define RMD_OTF(T, RR, CC)                                                                                     \
     do {                                                                                                       \

@@ -134,9 +134,7 @@ def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
     _require_gpu(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
-    compute = PRECISIONS[precision or _default_precision][0]
-    if compute == RMD_BF16X3:           # the on-the-fly kernels take exact f32 or bf16 operands
-        compute = RMD_F32
+    compute = PRECISIONS[precision or _default_precision][0]     # fp32: split bf16, fp32-exact: f32
     b, c, h, w = fmap1.shape
     ws = torch.ops.rmd.corr_otf_prepare(fmap1, fmap2, levels, compute, float(scale))
     return OtfState(ws, b, c, h, w, levels, compute)
