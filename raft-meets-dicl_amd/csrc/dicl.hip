@@ -1294,8 +1294,8 @@ dicl_stack_int_kernel(const float* __restrict__ f1, const float* __restrict__ f2
 // displacement planes re-read them), the channel loop unrolled by U so a lane's loads of U channels
 // are all in flight before its 2U stores, and optionally non-temporal stores (the 1.2 GB volume is
 // written once and read by the next kernel, never by this one).
-template <int CT, bool NT>
-__global__ void __launch_bounds__(kThreads)
+template <int CT, bool NT, int WPE = 1>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 dicl_stack_int_v2_kernel(const float* __restrict__ f1, const float* __restrict__ f2,
                          const unsigned char* __restrict__ nz, IntParams P, int nqb, int remap,
                          float* __restrict__ out) {
@@ -1348,7 +1348,7 @@ dicl_stack_int_v2_kernel(const float* __restrict__ f1, const float* __restrict__
 }
 
 // launch the integer volume (nz already computed); RMD_DICL_INT selects a variant for A/B runs
-// (tools/dicl_ab.py): 1 = the first kernel, 2 = plain stores, 3 = XCD remap.  Measured at cfg3
+// (tools/dicl_ab.py): 1 = the first kernel, 2 = plain stores, 3 = XCD remap, 4 = 8 waves per SIMD forced.  Measured at cfg3
 // (profiles/dicl_ab_r01.json): 0.366 ms (first) -> 0.234 ms (default: unrolled, nt, no remap)
 int launch_stack_int(const float* fmap1, const float* fmap2, const unsigned char* nz, const IntParams& P,
                      float* out, hipStream_t st) {
@@ -1365,7 +1365,8 @@ int launch_stack_int(const float* fmap1, const float* fmap2, const unsigned char
     RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack_int: grid too large");
     const bool nt = var != 2, remap = var == 3;
     if (P.C == 32) {
-        if (nt) dicl_stack_int_v2_kernel<32, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+        if (var == 4) dicl_stack_int_v2_kernel<32, true, 8><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+        else if (nt) dicl_stack_int_v2_kernel<32, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
         else dicl_stack_int_v2_kernel<32, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
     } else {
         dicl_stack_int_v2_kernel<0, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);

@@ -51,7 +51,7 @@ def main():
     g2 = torch.randn(b3, c3, h3, w3, generator=g).to(dev)
     g2[:, :, 10:20, 30:40] = 0
     nb3 = b3 * 49 * 2 * c3 * h3 * w3 * 4 + 2 * g1.numel() * 4
-    cases.append(("a8_int_cfg3", "RMD_DICL_INT", ["1", "0", "2", "3"], lambda: ops.dicl_stack_int(g1, g2, 3, 3), nb3))
+    cases.append(("a8_int_cfg3", "RMD_DICL_INT", ["1", "0", "2", "3", "4"], lambda: ops.dicl_stack_int(g1, g2, 3, 3), nb3))
     del out
     # backward (training): forward+backward minus forward; window variants (atomics: compare allclose)
     f1g, f2g, f2lg = (t.clone().requires_grad_(True) for t in (f1, f2, f2l))
