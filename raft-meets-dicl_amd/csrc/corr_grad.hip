@@ -245,7 +245,9 @@ grad_gemm_reduce(const float* __restrict__ ws, long long n, int splits, float* _
         }
         *reinterpret_cast<float4*>(out + i4) = s;
     } else {
-        for (long long i = i4; i < n; ++i) {
+        // scalar tail (n % 4 != 0, or the last partial group): this thread's 4 elements only
+        const long long iend = i4 + 4 < n ? i4 + 4 : n;
+        for (long long i = i4; i < iend; ++i) {
             float s = ws[i];
             for (int k = 1; k < splits; ++k) s += ws[(size_t)k * n + i];
             out[i] = s;
@@ -285,10 +287,10 @@ Plan plan(int batch, int M, int K, int Nc) {
 template <bool VA, bool VB, int LAYOUT>
 void launch_gemm(const GemmArgs& a, int nwg, hipStream_t st) {
     auto k = grad_gemm_x3<VA, VB, LAYOUT>;
-    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 kLdsA + kLdsB) == hipSuccess;
-    (void)attr;
+    // the >64 KB LDS opt-in is per device: set it before every launch (cheap host call), so a process
+    // that launches on a second GPU gets it too
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kLdsA + kLdsB);
     k<<<nwg, 512, kLdsA + kLdsB, st>>>(a);
 }
 
@@ -335,14 +337,18 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     g.ntn = pl.ntn;
     const long long nwg = (long long)pl.ntm * pl.ntn * pl.splits * batch;
     RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: grid too large");
-    const bool va = (lda & 3) == 0;
-    bool vb = (ldb & 3) == 0;
+    // float4 paths need 16-B aligned rows: row stride % 4 == 0 AND a 16-B aligned base pointer (a
+    // caller may pass an offset view); layouts 2 / 3 need only the base (4 consecutive elements of an
+    // 8-block are contiguous)
+    const bool a16 = ((uintptr_t)a & 15) == 0, b16 = ((uintptr_t)bm & 15) == 0;
+    const bool va = a16 && (lda & 3) == 0;
+    bool vb = b16 && (ldb & 3) == 0;
 #define RMD_GG(VA, VB)                                                                      \
     (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, st)                             \
      : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, st)                           \
      : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, st)                           \
                    : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, st))
-    if (layout >= 2) vb = true;                // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
+    if (layout >= 2) vb = b16;                 // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
     if (va && vb) RMD_GG(true, true);
     else if (va) RMD_GG(true, false);
     else if (vb) RMD_GG(false, true);

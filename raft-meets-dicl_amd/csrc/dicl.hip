@@ -2195,10 +2195,9 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
         hipStream_t st = as_stream(stream);
 #define RMD_DAPX3_R(MT, NW, AUX, KC, NB)                                                                    \
         do {                                                                                                \
-            static const bool attr = hipFuncSetAttribute(                                                   \
-                reinterpret_cast<const void*>(dap_x3_kernel<MT, NW, AUX, KC, NB>),                          \
-                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;                      \
-            (void)attr;                                                                                     \
+            /* the >64 KB LDS opt-in is per device: set before every launch */                           \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_x3_kernel<MT, NW, AUX, KC, NB>),     \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
             dap_x3_kernel<MT, NW, AUX, KC, NB><<<(unsigned)nwg, NW * 64, lds, st>>>(x, weight, disp, pixels, \
                                                                                   transpose, mblocks, per, out); \
         } while (0)

@@ -156,9 +156,20 @@ def _lookup_out(pyramid, coords, levels, radius):
     return coords.new_empty((b, levels * (2 * radius + 1) ** 2, h, w), dtype=torch.float32)
 
 
+def _check_device(name, *ts):
+    dev = ts[0].device
+    for t in ts[1:]:
+        if t.device != dev:
+            raise ValueError(f"{name}: tensors on different devices ({dev} / {t.device})")
+
+
 @_cuda("corr_lookup")
 def _corr_lookup(pyramid, coords, levels, radius, level_mask):
     b, two, h, w = coords.shape
+    if pyramid.dtype not in _STORAGE_CODE or pyramid.dim() != 1 or not pyramid.is_contiguous():
+        raise ValueError(f"corr_lookup: pyramid must be a contiguous 1-D float32/float16 tensor, got "
+                         f"{pyramid.dtype} {tuple(pyramid.shape)}")
+    _check_device("corr_lookup", pyramid, coords)
     d = describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype])
     if two != 2 or pyramid.numel() != d.total_elements:
         raise ValueError(f"corr_lookup: coords {tuple(coords.shape)} do not match the pyramid ({pyramid.numel()} elements)")
@@ -199,7 +210,16 @@ def _(fmap1, fmap2, levels, compute, scale):
 
 @_cuda("corr_otf_lookup")
 def _corr_otf_lookup(workspace, coords, channels, levels, compute, radius, level_mask):
-    b, _, h, w = coords.shape
+    b, two, h, w = coords.shape
+    # the workspace must be the one corr_otf_prepare built for these sizes and this compute mode: its
+    # segment layout depends on all of them, and the kernel trusts it
+    want = _lib.lib().rmd_corr_otf_workspace_bytes(b, channels, h, w, levels, compute)
+    if (two != 2 or workspace.dtype != torch.uint8 or workspace.dim() != 1 or not workspace.is_contiguous()
+            or want == 0 or workspace.numel() != want):
+        raise ValueError(f"corr_otf_lookup: workspace ({workspace.dtype}, {workspace.numel()} B) does not match "
+                         f"coords {tuple(coords.shape)}, channels={channels}, levels={levels}, compute={compute} "
+                         f"({want} B expected)")
+    _check_device("corr_otf_lookup", workspace, coords)
     co = _f32(coords)
     out = _lookup_out(workspace, co, levels, radius)
     with _Dev(co) as st:

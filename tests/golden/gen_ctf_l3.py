@@ -16,10 +16,15 @@ test regenerates the same weights on tests/e2e/ctf_l3_net.CtfL3Net) and stores o
       (lr 4e-4, weight decay 1e-4, eps 1e-8: the train/chairs2-1 stage); stores the loss, the total
       gradient norm, every parameter's gradient norm, and the loss of a second forward after the step.
 
+  ctf_l3_fwd_376x1242.npz  (6b at the cfg4 size) the same inference fixture for a KITTI-shape
+      376x1242 pair padded to 384x1280 (cfg/model/raft+dicl-ctf3l.yaml:26-33), BASELINE configs[3].
+  ctf_l3_train_b6_384x512.npz  (7 at the benched batch) the training step with the cfg5 per-GPU
+      batch 6 (pairs: the two of the batch-2 fixture plus four more seeded textures and flows).
+
 Before writing, the restatement tests/e2e/ctf_l3_net.py (given the reference's own make_cmod) is
 checked against the reference forward and loss: they must agree bitwise on the CPU.
 
-usage: python tests/golden/gen_ctf_l3.py
+usage: python tests/golden/gen_ctf_l3.py [fwd512] [train] [fwd1242] [train6]   (default: all)
 """
 
 import os
@@ -49,11 +54,15 @@ def sample_pixels(h, w, n, seed=7):
     return np.sort(rng.choice(h * w, n, replace=False))
 
 
-def train_batch():
-    """Two synthetic pairs (different textures and flows) + padded targets and validity masks."""
+# (texture seed, integer flow) of the training pairs; batch n takes the first n
+TRAIN_PAIRS = ((1234, (3, 5)), (99, (6, 2)), (7, (2, 4)), (21, (5, 1)), (314, (1, 6)), (2718, (4, 3)))
+
+
+def train_batch(n=2):
+    """n synthetic pairs (different textures and flows) + padded targets and validity masks."""
     import torch
     imgs1, imgs2, flows, valids = [], [], [], []
-    for seed, flow in ((1234, (3, 5)), (99, (6, 2))):
+    for seed, flow in TRAIN_PAIRS[:n]:
         i1, i2, gt = frame_pair(H, W, flow=flow, seed=seed, pad=PAD)
         hp, wp = i1.shape[-2:]
         f = np.zeros((1, 2, hp, wp), np.float32)
@@ -82,23 +91,24 @@ def train_step(model, loss_fn, freeze, img1, img2, flow, valid):
     return float(loss), total, names, gnorm, float(loss1)
 
 
-def main():
+def _models():
     import torch
     mods = _import_reference()  # noqa: F841
     from src.models.impls import raft_dicl_ctf_l3 as ctf
-    from src.models.common import corr as rcorr, norm as rnorm
-    from src.models.common.loss import mlseq
-    from e2e.ctf_l3_net import CtfL3Net, freeze_batchnorm, mlseq_loss
+    from src.models.common import corr as rcorr
+    from e2e.ctf_l3_net import CtfL3Net
     torch.manual_seed(0)
     torch.set_num_threads(os.cpu_count() or 8)
-
     ref = det_init_fanin(ctf.RaftPlusDiclModule(), head_gain=HEAD_GAIN)
     mine = det_init_fanin(CtfL3Net(rcorr.make_cmod, rcorr.make_flow_regression), head_gain=HEAD_GAIN)
     assert sorted(ref.state_dict().keys()) == sorted(mine.state_dict().keys())
-    ref_loss = mlseq.MultiLevelSequenceLoss({"ord": 1, "gamma": 0.85, "alpha": (0.38, 0.6, 1.0)})
+    return ref, mine
 
-    # ---- (6b) inference ----------------------------------------------------------------------
-    img1, img2, gt = frame_pair(H, W, pad=PAD)
+
+def gen_forward(ref, mine, h, w, name):
+    """(6b) inference at h x w padded to PAD, eval mode, iterations ITERS."""
+    import torch
+    img1, img2, gt = frame_pair(h, w, pad=PAD)
     i1, i2 = torch.from_numpy(img1), torch.from_numpy(img2)
     ref.eval(), mine.eval()
     with torch.no_grad():
@@ -108,38 +118,59 @@ def main():
         for a, b in zip(lr_, lm):
             assert torch.equal(a, b), float((a - b).abs().max())
     print("restatement == reference (forward, bitwise)")
-    sel = sample_pixels(H, W, SAMPLES)
-    arrays = dict(height=np.int32(H), width=np.int32(W), pad=np.int32(PAD), iterations=np.asarray(ITERS, np.int32),
+    sel = sample_pixels(h, w, SAMPLES)
+    arrays = dict(height=np.int32(h), width=np.int32(w), pad=np.int32(PAD), iterations=np.asarray(ITERS, np.int32),
                   pixels=sel, keys=np.asarray(sorted(ref.state_dict().keys())),
                   epe3=np.asarray([epe(f.numpy(), gt) for f in out_r[2]]))
-    for lvl, name in ((0, "flow5"), (1, "flow4")):
-        arrays[name] = np.stack([f.numpy() for f in out_r[lvl]]).astype(np.float32)
+    for lvl, nm in ((0, "flow5"), (1, "flow4")):
+        arrays[nm] = np.stack([f.numpy() for f in out_r[lvl]]).astype(np.float32)
     for k, f in enumerate(out_r[2]):
-        f = f.numpy()[0, :, :H, :W].reshape(2, -1)
+        f = f.numpy()[0, :, :h, :w].reshape(2, -1)
         assert np.isfinite(f).all()
         arrays[f"flow3_it{k}"] = f[:, sel].astype(np.float32)
-    path = os.path.join(HERE, "ctf_l3_fwd_384x512.npz")
+    path = os.path.join(HERE, name)
     np.savez_compressed(path, **arrays)
     print(path, os.path.getsize(path), "bytes; EPE (1/8 level):", np.round(arrays["epe3"], 4).tolist(),
           "flow5 range", float(np.abs(arrays["flow5"]).max()))
 
-    # ---- (7) one training step ---------------------------------------------------------------
-    b1, b2, fl, va = train_batch()
+
+def gen_train(ref, mine, n, name):
+    """(7) one training step at cfg5 shape with batch n."""
+    from src.models.common import norm as rnorm
+    from src.models.common.loss import mlseq
+    from e2e.ctf_l3_net import freeze_batchnorm, mlseq_loss
+    ref_loss = mlseq.MultiLevelSequenceLoss({"ord": 1, "gamma": 0.85, "alpha": (0.38, 0.6, 1.0)})
+    b1, b2, fl, va = train_batch(n)
     res_r = train_step(ref, lambda r, f, v: ref_loss(None, r, f, v), lambda m: rnorm.freeze_batchnorm(m, True),
                        b1, b2, fl, va)
     res_m = train_step(mine, mlseq_loss, freeze_batchnorm, b1, b2, fl, va)
     assert res_r[0] == res_m[0] and res_r[1] == res_m[1] and res_r[4] == res_m[4], (res_r[0], res_m[0])
-    assert res_r[2] == res_m[2] and all(res_r[3][n] == res_m[3][n] for n in res_r[2])
+    assert res_r[2] == res_m[2] and all(res_r[3][k] == res_m[3][k] for k in res_r[2])
     print("restatement == reference (training step: loss, gradient norms, loss after AdamW, bitwise)")
     loss0, total, names, gnorm, loss1 = res_r
-    path = os.path.join(HERE, "ctf_l3_train_384x512.npz")
-    np.savez_compressed(path, height=np.int32(H), width=np.int32(W), pad=np.int32(PAD), batch=np.int32(2),
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, height=np.int32(H), width=np.int32(W), pad=np.int32(PAD), batch=np.int32(n),
                         iterations=np.asarray(ITERS, np.int32), loss=np.float64(loss0), grad_norm=np.float64(total),
-                        names=np.asarray(names), grad_norms=np.asarray([gnorm[n] for n in names]),
+                        names=np.asarray(names), grad_norms=np.asarray([gnorm[k] for k in names]),
                         loss_after_step=np.float64(loss1), lr=np.float64(OPT["lr"]),
-                        weight_decay=np.float64(OPT["weight_decay"]), eps=np.float64(OPT["eps"]))
+                        weight_decay=np.float64(OPT["weight_decay"]), eps=np.float64(OPT["eps"]),
+                        pair_seeds=np.asarray([p[0] for p in TRAIN_PAIRS[:n]], np.int64),
+                        pair_flows=np.asarray([p[1] for p in TRAIN_PAIRS[:n]], np.int64))
     print(path, os.path.getsize(path), "bytes; loss", loss0, "grad norm", total, "loss after step", loss1,
           "params with grads", len(names))
+
+
+def main():
+    which = set(sys.argv[1:]) or {"fwd512", "train", "fwd1242", "train6"}
+    # every fixture starts from freshly initialised weights (a training step changes them)
+    if "fwd512" in which:
+        gen_forward(*_models(), H, W, "ctf_l3_fwd_384x512.npz")
+    if "train" in which:
+        gen_train(*_models(), 2, "ctf_l3_train_384x512.npz")
+    if "fwd1242" in which:
+        gen_forward(*_models(), 376, 1242, "ctf_l3_fwd_376x1242.npz")
+    if "train6" in which:
+        gen_train(*_models(), 6, "ctf_l3_train_b6_384x512.npz")
 
 
 if __name__ == "__main__":

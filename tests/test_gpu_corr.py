@@ -307,12 +307,14 @@ def _gemm_operand(bl, layout):
 
 
 @pytest.mark.parametrize("layout", [0, 1, 2, 3])
-@pytest.mark.parametrize("b,m,k,nc", [(6, 256, 3790, 2852), (2, 100, 37, 45), (1, 300, 129, 130), (3, 32, 1000, 7)])
+@pytest.mark.parametrize("b,m,k,nc", [(6, 256, 3790, 2852), (2, 100, 37, 45), (1, 300, 129, 130), (3, 32, 1000, 7),
+                                     (1, 33, 4096, 35)])
 def test_corr_grad_gemm_vs_fp64(layout, b, m, k, nc):
     """rmd_corr_grad_gemm (split-bf16 x3 MFMA) against a float64 GEMM, elementwise, in all four B
     layouts (2 / 3: the 8-target blocked order of the pyramid gradient).  Shapes: the cfg5 backward
     (B6, C256, T = 3790 pooled targets, N = 2852 queries; lda = 3790 is not 16-B aligned), ragged
-    tiles and 8-blocks, M over two 256-row tiles, a K split into several workgroups."""
+    tiles and 8-blocks, M over two 256-row tiles, a K split into several workgroups; (1, 33, 4096, 35)
+    splits K and has batch*m*nc % 4 != 0 (the split-K reduction's scalar tail)."""
     import ctypes
     from rmd import _lib
     g = torch.Generator(device="cpu").manual_seed(m + k)
@@ -332,6 +334,33 @@ def test_corr_grad_gemm_vs_fp64(layout, b, m, k, nc):
     # fp32-accurate: |err| <= 2e-5 * sqrt(k) * rms(|a||b|) — the dropped lo.lo term and fp32 accumulation
     tol = 2e-5 * np.sqrt(k) + 1e-6
     assert_close_elementwise(got.numpy(), ref.numpy(), rtol=1e-4, atol=tol)
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+def test_corr_grad_gemm_misaligned_base_pointers(layout):
+    """The C ABI takes plain strided pointers: operands that start 4 B past a 16-B boundary (an offset
+    view) must take the scalar load path, not misaligned float4 loads."""
+    import ctypes
+    from rmd import _lib
+    b, m, k, nc = 2, 70, 136, 72
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = torch.randn(b, m, k, generator=g)
+    bl = torch.randn(b, k, nc, generator=g)
+    ref = torch.bmm(a.double(), bl.double())
+    bm, ldb = _gemm_operand(bl, layout)
+    lib = _lib.lib()
+    abuf = torch.zeros(a.numel() + 4, device=DEV)
+    bbuf = torch.zeros(bm.numel() + 4, device=DEV)
+    abuf[1:1 + a.numel()] = a.reshape(-1).to(DEV)
+    bbuf[1:1 + bm.numel()] = bm.reshape(-1).to(DEV)
+    out = torch.full((b, m, nc), float("nan"), device=DEV)
+    ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, m, k, nc), 1), dtype=torch.uint8, device=DEV)
+    rc = lib.rmd_corr_grad_gemm(ctypes.c_void_p(abuf.data_ptr() + 4), k, ctypes.c_void_p(bbuf.data_ptr() + 4), ldb,
+                                b, m, k, nc, layout, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert_close_elementwise(out.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=2e-5 * np.sqrt(k) + 1e-6)
 
 
 @pytest.mark.parametrize("b,h,w", [(1, 55, 128), (2, 40, 64), (1, 23, 96), (3, 55, 128), (1, 46, 62)])

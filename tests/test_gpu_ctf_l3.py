@@ -9,10 +9,10 @@ GPU) and its convex upsampling rmd.raft.Up8Network.  Weights: detinit.det_init_f
 flow head gain 0.02), regenerated here.
 
 Tolerances:
-  * inference (384x512 b1, iterations (4, 3, 3)): |EPE - EPE_ref| <= 1e-3 px for every 1/8-level
+  * inference (384x512 and 376x1242 -> 384x1280, b1, iterations (4, 3, 3)): |EPE - EPE_ref| <= 1e-3 px for every 1/8-level
     output (north_star's EPE gate); 1/32 and 1/16 flows of every iteration and sampled full-resolution
     flows within 1e-2 px (MIOpen vs CPU ATen convolutions: summation order only).
-  * training step (cfg5 shape 384x512, batch 2, mlseq loss, clip 1.0, AdamW): loss and total gradient
+  * training step (cfg5 shape 384x512, batch 2 and 6, mlseq loss, clip 1.0, AdamW): loss and total gradient
     norm within 1e-4 relative; every parameter's gradient norm within 1e-3 relative, except gradients
     that are zero in exact arithmetic and rounding noise in both runs (biases of convolutions followed
     by InstanceNorm, e.g. fnet.conv1.bias: ~1e-6 against a total norm of ~2.6e3), which must stay below
@@ -54,8 +54,10 @@ def _report(name, rep):
             json.dump(rep, fh)
 
 
-def test_ctf_l3_forward_matches_reference():
-    g = load_golden("ctf_l3_fwd_384x512")
+@pytest.mark.parametrize("fixture", ["ctf_l3_fwd_384x512", "ctf_l3_fwd_376x1242"])
+def test_ctf_l3_forward_matches_reference(fixture):
+    """384x512 (cfg5 frame) and the cfg4 KITTI shape 376x1242 padded to 384x1280 (BASELINE configs[3])."""
+    g = load_golden(fixture)
     h, w, pad = int(g["height"]), int(g["width"]), int(g["pad"])
     iters = tuple(int(i) for i in g["iterations"])
     net = _net().eval()
@@ -71,14 +73,14 @@ def test_ctf_l3_forward_matches_reference():
              for k, f in enumerate(flows))
     rep = {"epe_ref": g["epe3"].tolist(), "epe": [epe(f, gt) for f in flows], "max_abs_epe_diff": max(d_epe),
            "max_flow_diff_px": {"1/32": d5, "1/16": d4, "full": d3}}
-    _report("ctf_l3_forward", rep)
+    _report(fixture, rep)
     assert max(d_epe) <= 1e-3, rep
     assert max(d5, d4, d3) <= 1e-2, rep
 
 
-def _train_batch(h, w, pad):
+def _train_batch(h, w, pad, pairs):
     imgs1, imgs2, flows, valids = [], [], [], []
-    for seed, flow in ((1234, (3, 5)), (99, (6, 2))):
+    for seed, flow in pairs:
         i1, i2, gt = frame_pair(h, w, flow=flow, seed=seed, pad=pad)
         hp, wp = i1.shape[-2:]
         f = np.zeros((1, 2, hp, wp), np.float32)
@@ -89,11 +91,18 @@ def _train_batch(h, w, pad):
     return [torch.from_numpy(np.concatenate(x)).cuda() for x in (imgs1, imgs2, flows, valids)]
 
 
-def test_ctf_l3_training_step_matches_reference():
-    g = load_golden("ctf_l3_train_384x512")
+@pytest.mark.parametrize("fixture", ["ctf_l3_train_384x512", "ctf_l3_train_b6_384x512"])
+def test_ctf_l3_training_step_matches_reference(fixture):
+    """cfg5 shape at batch 2 and at the benched per-GPU batch 6."""
+    g = load_golden(fixture)
     h, w, pad = int(g["height"]), int(g["width"]), int(g["pad"])
     iters = tuple(int(i) for i in g["iterations"])
-    img1, img2, flow, valid = _train_batch(h, w, pad)
+    if "pair_seeds" in g:
+        pairs = [(int(s), tuple(int(v) for v in f)) for s, f in zip(g["pair_seeds"], g["pair_flows"])]
+    else:
+        pairs = [(1234, (3, 5)), (99, (6, 2))]
+    assert len(pairs) == int(g["batch"])
+    img1, img2, flow, valid = _train_batch(h, w, pad, pairs)
     net = _net()
     net.train()
     freeze_batchnorm(net)
@@ -125,7 +134,7 @@ def test_ctf_l3_training_step_matches_reference():
            "zero_gradient_params": [names[i] for i in np.nonzero(zero)[0]],
            "loss_after_step": loss1, "loss_after_step_ref": float(g["loss_after_step"]),
            "loss_after_step_rel_diff": abs(loss1 - float(g["loss_after_step"])) / abs(float(g["loss_after_step"]))}
-    _report("ctf_l3_train_step", rep)
+    _report(fixture, rep)
     assert rep["loss_rel_diff"] <= 1e-4, rep
     assert rep["grad_norm_rel_diff"] <= 1e-4, rep
     assert ok_gn.all(), [(names[i], gn[i], ref_gn[i]) for i in np.nonzero(~ok_gn)[0][:10]]

@@ -66,6 +66,37 @@ def test_dicl_ml_level_stacks_golden(dap_type):
         assert rel_max_err(st.cpu().numpy(), g[f"stack_{i}"]) < 1e-5
 
 
+@pytest.mark.parametrize("kind,fixture", [("dicl-1x1", "dicl1x1_b2_c16_8x12"), ("dicl-emb", "diclemb_b2_c16_8x12")])
+def test_dicl_variant_module_golden_forward_and_gradients(kind, fixture):
+    """Whole 'dicl-1x1' / 'dicl-emb' modules (corr/dicl_1x1.py:33-86, corr/dicl_emb.py:32-104) in train
+    mode against the reference's outputs: MatchingNet output (hook), module output and the gradients of
+    a seeded upstream gradient w.r.t. both feature maps, with and without DAP, and w.r.t. every
+    parameter (dap=True).  Our stack kernel feeds MIOpen convolutions here, so the gradient tolerances
+    cover MIOpen's fp32 algorithms (forward 1e-4, feature gradients 2e-4, parameter gradients 1e-3)."""
+    import rmd
+    g = load_golden(fixture)
+    mod = rmd.corr.make_cmod(kind, 16, int(g["radius"]), dap_init="standard")
+    assert sorted(mod.state_dict().keys()) == sorted(g["sd.keys"].tolist())
+    det_init(mod)
+    mod = mod.to(DEV).train()
+    for dap in (True, False):
+        tag = "dap" if dap else "nodap"
+        cap = {}
+        hook = mod.mnet.register_forward_hook(lambda m, i, o: cap.update(cost=o))
+        f1, f2 = _t(g["fmap1"], True), _t(g["fmap2"], True)
+        out = mod(f1, f2, _t(g["coords"]), dap=dap)
+        hook.remove()
+        assert tuple(out.shape) == g[f"{tag}.out"].shape
+        assert rel_max_err(cap["cost"].detach().cpu().numpy(), g[f"{tag}.cost"]) < 1e-4
+        assert rel_max_err(out.detach().cpu().numpy(), g[f"{tag}.out"]) < 1e-4
+        params = [(k, p) for k, p in mod.named_parameters()] if dap else []
+        grads = torch.autograd.grad(out, [f1, f2] + [p for _, p in params], _t(g[f"{tag}.grad_out"]))
+        assert rel_max_err(grads[0].cpu().numpy(), g[f"{tag}.grad_fmap1"]) < 2e-4
+        assert rel_max_err(grads[1].cpu().numpy(), g[f"{tag}.grad_fmap2"]) < 2e-4
+        for (k, _), gp in zip(params, grads[2:]):
+            assert rel_max_err(gp.cpu().numpy(), g[f"{tag}.pg.{k}"]) < 1e-3, k
+
+
 def test_dicl_emb_stack_has_delta_channels():
     import rmd
     g = load_golden("dicl_b1_c16_8x12")

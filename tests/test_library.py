@@ -72,3 +72,15 @@ def test_opcheck_operator_families():
     pyr = torch.ops.rmd.corr_pyramid(f1.detach(), f2.detach(), 3, _lib.RMD_BF16X3, _lib.RMD_F32, 0.25)
     torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0),
                           test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+
+
+@pytest.mark.parametrize("kind,fixture", [("dicl", "dicl_b1_c16_8x12"), ("dicl-1x1", "dicl1x1_b2_c16_8x12"),
+                                          ("dicl-emb", "diclemb_b2_c16_8x12")])
+def test_correlation_module_state_dict_keys_match_reference(kind, fixture):
+    """The drop-in modules keep the reference's state-dict keys (checkpoints load unchanged): compared
+    with the keys the reference module had when the fixture was generated (CPU, no kernels run)."""
+    import rmd
+    from conftest import load_golden
+    g = load_golden(fixture)
+    mod = rmd.corr.make_cmod(kind, 16, int(g["radius"]), dap_init="standard")
+    assert sorted(mod.state_dict().keys()) == sorted(g["sd.keys"].tolist())
