@@ -58,9 +58,16 @@ def parse():
     ap.add_argument("--event-every", type=int, default=5,
                     help="record the per-kernel HIP events (roofline) on every E-th timed step "
                          "(steps E-1, 2E-1, ...: never the first timed step)")
-    ap.add_argument("--model-level", choices=["auto", "on", "off"], default="auto",
-                    help="also time the whole RAFT network (436x1024 b8, 12 iterations) with the rmd path "
-                         "(extra key; auto = single-GPU runs only)")
+    ap.add_argument("--model-level", choices=["on", "off"], default="on",
+                    help="also time the whole RAFT network (436x1024, 12 iterations) with the rmd path on every "
+                         "rank, batch-sharded like the headline (extra key 'model_level')")
+    ap.add_argument("--fp32-mode", choices=["on", "off"], default="on",
+                    help="extra key 'fp32_mode': the headline step in the fp32 parity mode (x3 GEMM, fp32 "
+                         "pyramid) on the same inputs, with its own rooflines")
+    ap.add_argument("--fp32-steps", type=int, default=10)
+    ap.add_argument("--live-pmc", choices=["on", "off"], default="on",
+                    help="rank 0 of single-GPU runs: roofline traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes "
+                         "over tools/pmc_probe.py run as child processes in this run")
     ap.add_argument("--train", choices=["on", "off"], default="on",
                     help="also time the cfg5 training step (RAFT+DICL ctf-l3, DDP over RCCL when N > 1): "
                          "extra key 'train_step'")
@@ -153,17 +160,49 @@ def cpu_baseline(args):
     finally:
         torch.set_num_threads(prev)
     med = float(np.median(times))
+    comps = cpu_components(threads, args.cpu_budget_s)
     return {"value": 1.0 / med, "unit": "frame-pairs/s", "cores": threads, "kind": "port",
-            "ms_per_pair": med * 1e3, "runs": len(times),
+            "ms_per_pair": med * 1e3, "runs": len(times), "components_cfg2_b1": comps,
             "sample": f"BASELINE configs[0]: whole RAFT network (raft/baseline, 12 iterations) on one synthetic "
                       f"368x496 pair, batch 1, fp32 torch-CPU with the reference's eager correlation "
                       f"(tests/e2e/eager_corr.py); 1 warm-up + median of {len(times)}"}
 
 
-def model_level(rank_dev, precision):
-    """Context for the headline (not `value`): the whole RAFT network at 436x1024 (padded 440x1024),
-    batch 8, 12 iterations, MIOpen fp32 convolutions, with rmd.raft.CorrBlock + rmd.raft.Up8Network
-    (tools/bench_e2e.py compares it with the eager reference correlation)."""
+def cpu_components(threads, budget_s):
+    """BASELINE.md §3 / SURVEY.md §8(d) 'CPU beside GPU': the reference correlation's two components at
+    cfg2 shape with batch 1 (55x128 feature maps, C=256) on torch-CPU — the all-pairs GEMM + pyramid
+    build (raft.py:18-47) and one radius-4 lookup (raft.py:49-95) — through the op-for-op restatement
+    tests/e2e/eager_corr.EagerCorrBlock (test infrastructure); 1 warm-up + median of up to 5."""
+    from e2e.eager_corr import EagerCorrBlock
+    f1, f2, coords = synthetic(1, 256, 55, 128, 12, 1234, "cpu")
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        tp, tl = [], []
+        with torch.no_grad():
+            for k in range(6):
+                t0 = time.perf_counter()
+                cb = EagerCorrBlock(f1, f2, 4, 4)
+                t1 = time.perf_counter()
+                cb(coords[k % 12])
+                t2 = time.perf_counter()
+                if k:
+                    tp.append(t1 - t0)
+                    tl.append(t2 - t1)
+                if k and sum(tp) + sum(tl) > budget_s:
+                    break
+    finally:
+        torch.set_num_threads(prev)
+    return {"pyramid_ms": float(np.median(tp)) * 1e3, "lookup_ms": float(np.median(tl)) * 1e3, "cores": threads,
+            "runs": len(tp), "kind": "port",
+            "sample": "cfg2 shape, batch 1 (55x128, C=256, 4 levels, r=4): EagerCorrBlock constructor (GEMM + "
+                      "avg-pool pyramid, raft.py:18-47) and one lookup (raft.py:49-95), fp32 torch-CPU"}
+
+
+def model_level(rank_dev, precision, b=8, rank=0, dry_run=False):
+    """The whole RAFT network at 436x1024 (padded 440x1024), batch b, MIOpen fp32 convolutions, with
+    rmd.raft.CorrBlock + rmd.raft.Up8Network (tools/bench_e2e.py compares it with the eager reference
+    correlation): network and a synthetic batch on the rank's device."""
     import torch.nn.functional as F
     for p in (os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
         if p not in sys.path:
@@ -173,27 +212,59 @@ def model_level(rank_dev, precision):
     from e2e.raft_net import RaftNet
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
-    b, h, w = 8, 440, 1024
-    g = torch.Generator().manual_seed(1234)
+    h, w = (128, 128) if dry_run else (440, 1024)      # dry run: level 3 is 2x2 (a 1-pixel level is NaN)
+    g = torch.Generator().manual_seed(1234 + rank)
     low = torch.rand(b, 3, h // 8, w // 8, generator=g) * 2 - 1
     img1 = F.interpolate(low, size=(h, w), mode="bilinear", align_corners=True).to(rank_dev)
     img2 = torch.roll(img1, shifts=(3, 5), dims=(2, 3))
-    net = det_init_fanin(RaftNet(rmd.raft.CorrBlock, precision=precision, upnet_cls=rmd.raft.Up8Network))
+    if dry_run:
+        # --dry-run (CPU gloo tests): a small frame through the eager reference correlation on the CPU,
+        # exercising the shard / seed / MAX-over-ranks plumbing of the leg, not the kernels
+        from e2e.eager_corr import EagerCorrBlock
+        net = det_init_fanin(RaftNet(EagerCorrBlock))
+    else:
+        net = det_init_fanin(RaftNet(rmd.raft.CorrBlock, precision=precision, upnet_cls=rmd.raft.Up8Network))
     net = net.eval().to(rank_dev)
+    return net, img1, img2
+
+
+def model_leg(args, world, rank, device):
+    """BASELINE.md frame-pairs/s of the 'cfg2 model at 1/2/4/8 GPUs': the whole RAFT network at
+    436x1024 (padded 440x1024), 12 iterations, on every rank with its own batch shard (per-GPU b8, or
+    --global-batch split), no collective on the data path; job time = MAX over ranks."""
+    b = args.global_batch // world if args.global_batch else args.batch
+    net, img1, img2 = model_level(device, args.precision, b, rank, args.dry_run)
+    reps = 1 if args.dry_run else 3
+    iters = 2 if args.dry_run else 12
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
     with torch.no_grad():
-        for _ in range(2):
-            net(img1, img2, 12)
-        torch.cuda.synchronize(rank_dev)
+        for i in range(1 if args.dry_run else 2):
+            net(img1, img2, iters)
+            progress(rank, f"model_level warm-up {i + 1}")
+        sync()
+        if world > 1:
+            torch.distributed.barrier()
+        sync()
         t0 = time.perf_counter()
-        reps = 3
         for _ in range(reps):
-            net(img1, img2, 12)
-        torch.cuda.synchronize(rank_dev)
-    ms = (time.perf_counter() - t0) * 1e3 / reps
-    del net
+            out = net(img1, img2, iters)
+        sync()
+        el = time.perf_counter() - t0
+        shard_sum = float(out[-1].double().sum())
+    if world > 1:
+        torch.distributed.barrier()
+    el = job_time(el, world, device)
+    del net, img1, img2
     torch.cuda.empty_cache()
-    return {"frame_pairs_per_s": b * 1e3 / ms, "ms_per_batch": ms, "batch": b, "iterations": 12,
-            "precision": precision, "convs": "MIOpen fp32 (TF32 off)",
+    return {"frame_pairs_per_s": world * b * reps / el, "ms_per_batch": el / reps * 1e3, "per_gpu_batch": b,
+            "global_batch": world * b, "n_gpus": world, "iterations": iters, "precision": args.precision,
+            "rank0_flow_checksum": shard_sum,
+            "parallelism": f"batch-shard x{world} (no collective)",
+            "scaling": "strong" if args.global_batch else "weak", "convs": "MIOpen fp32 (TF32 off)",
             "workload": "whole RAFT network 436x1024 (padded 440x1024): encoders + GRU + rmd correlation + rmd Up8"}
 
 
@@ -463,32 +534,24 @@ def init_distributed(args):
     return world, rank, device
 
 
-def main():
-    args = parse()
-    maybe_launch(args)
-    world, rank, device = init_distributed(args)
-    H, W = padded(args.height, args.width)
-    h8, w8 = H // 8, W // 8
-    if args.global_batch:
-        if args.global_batch % world:
-            raise SystemExit(f"bench.py: --global-batch {args.global_batch} is not a multiple of {world} ranks")
-        args.batch = args.global_batch // world
-    B = args.batch
-    N = h8 * w8
-    D = (2 * args.radius + 1) ** 2
+HBM_COPY_GBS = 6290.0          # measured float4 copy rate (MI355X_MICROARCH.md chip table)
 
-    ev_gemm = []      # (start, end) around the GEMM launch alone (rmd_corr_pyramid_prepared)
-    ev_look = []      # (start, end) around the 12 lookup launches of a step
+
+def corr_leg(args, precision, inputs, world, device, steps, warmup):
+    """Time `steps` hot-path steps (operand prep + correlation GEMM + `iters` lookups) after `warmup`
+    untimed ones, bracketed by barrier + synchronize, job time = MAX over ranks; HIP events on the launch
+    stream around the GEMM launch alone and around the lookups of every E-th timed step (never the first)."""
+    ev_gemm, ev_look = [], []
     if args.dry_run:
         def step(record):
             return None
     else:
         from rmd import ops
-        f1, f2, coords = rank_inputs(args, rank, world, h8, w8, device)
+        f1, f2, coords = inputs
         stream = torch.cuda.current_stream(device)
 
         def step(record):
-            pyr = ops.corr_pyramid(f1, f2, args.levels, args.precision, events=ev_gemm if record else None)
+            pyr = ops.corr_pyramid(f1, f2, args.levels, precision, events=ev_gemm if record else None)
             if record:
                 a = torch.cuda.Event(enable_timing=True)
                 z = torch.cuda.Event(enable_timing=True)
@@ -505,7 +568,7 @@ def main():
         if not args.dry_run:
             torch.cuda.synchronize(device)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(False)
     sync()
     if world > 1:
@@ -513,13 +576,151 @@ def main():
     sync()
     E = max(1, args.event_every)
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         step(i % E == E - 1)
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         torch.distributed.barrier()
-    elapsed = job_time(elapsed, world, device)
+    return job_time(elapsed, world, device), ev_gemm, ev_look
+
+
+def live_traffic(args, precision, batch, rank):
+    """HBM bytes per launch of the GEMM and lookup kernels from rocprofv3 PMC counters collected in THIS
+    run: separate FETCH_SIZE and WRITE_SIZE passes (one counter group each, MI355X_MICROARCH.md HBM /
+    PMC sections) over tools/pmc_probe.py (the same step on the same synthetic inputs), each a child
+    process under its own KILL timeout.  gfx950 corrections: both counters are KiB; FETCH_SIZE counts
+    half the bytes of wide streaming reads, so it is doubled.  Returns ({kernel: bytes}, note)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not on PATH"
+    d = tempfile.mkdtemp(prefix="rmd_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    per = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = os.path.join(d, counter.lower())
+        cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "run",
+               "--", sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), "--precision", precision,
+               "--batch", str(batch), "--height", str(args.height), "--width", str(args.width),
+               "--channels", str(args.channels), "--iters", str(args.iters)]
+        progress(rank, f"live PMC pass {counter} ({precision})")
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=d)
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            shutil.rmtree(d, ignore_errors=True)
+            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode}): {r.stderr.decode()[-200:]}"
+        vals = {}
+        for row in csv.DictReader(open(files[0])):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row["Kernel_Name"]
+            key = "gemm" if "corr_pyramid_" in name else "lookup" if "corr_lookup_kernel" in name else None
+            if key:
+                vals.setdefault(key, []).append(float(row["Counter_Value"]) * 1024.0)
+        for k, v in vals.items():
+            per.setdefault(k, {})[counter] = (sum(v) / len(v), len(v))
+    shutil.rmtree(d, ignore_errors=True)
+    res = {}
+    for k, c in per.items():
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            res[k] = {"read": 2.0 * c["FETCH_SIZE"][0], "write": c["WRITE_SIZE"][0],
+                      "total": 2.0 * c["FETCH_SIZE"][0] + c["WRITE_SIZE"][0], "dispatches": c["FETCH_SIZE"][1]}
+    return res, "live: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (KiB -> B, gfx950 correction), this run, tools/pmc_probe.py"
+
+
+def stored_traffic(precision):
+    """Counter bytes of an earlier profiled run (profiles/pmc_r02.json) — only where no live pass ran."""
+    for name in ("pmc_r02.json", "pmc_r01.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(path):
+            try:
+                with open(path) as fh:
+                    e = json.load(fh).get(precision, {})
+            except (OSError, ValueError):
+                continue
+            det = e.get("detail", {})
+            res = {k: {"read": v.get("fetch_bytes"), "write": v.get("write_bytes"), "total": v.get("hbm_bytes_per_launch")}
+                   for k, v in det.items() if k in ("gemm", "lookup")}
+            if res:
+                return res, f"stored: profiles/{name} (an earlier box and tree; no live pass in this run)"
+    return {}, "none"
+
+
+def rooflines(args, precision, B, h8, w8, gemm_ms, look_ms, traffic, traffic_note, n_gemm, n_look):
+    """roofline dicts of the GEMM and of the lookup from their average launch times (algorithmic bytes /
+    flops per launch) and the counter traffic."""
+    from rmd import _lib, ops
+    N = h8 * w8
+    D = (2 * args.radius + 1) ** 2
+    s = 2 if precision in ("bf16", "fp32-f16") else 4
+    compute_dt = "fp32" if precision.startswith("fp32") else "bf16"
+    levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
+    look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
+    op_bytes = 2 if precision.startswith("bf16") else 4
+    gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
+    gemm_flop = 2.0 * B * N * N * args.channels
+    # MFMA work actually issued: the fp32 mode runs three bf16 products per k-step (x3 kernel)
+    mfma_dt, mfma_mult = ("bf16", 3.0) if precision == "fp32" else (compute_dt, 1.0)
+    look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
+    gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
+    gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
+    traffic = traffic or {}
+    kname = _lib.lib().rmd_corr_gemm_kernel(_lib.describe(B, h8, w8, args.levels, ops.PRECISIONS[precision][1]),
+                                             args.channels, ops.PRECISIONS[precision][0]).decode()
+
+    def tr(k, key):
+        v = traffic.get(k, {}).get(key)
+        return float(v) if v is not None else None
+
+    gt, lt = tr("gemm", "total"), tr("lookup", "total")
+    # MFMA fraction the HBM store stream allows: the algorithmic bytes moved at the measured copy rate
+    # (and at the 8 TB/s spec) bound the launch time from below, so the flops over that time bound MFMA
+    ceil = {r: gemm_flop * mfma_mult / (gemm_bytes / (gbs * 1e9)) / 1e12 / MFMA_PEAK[mfma_dt]
+            for r, gbs in (("copy_rate", HBM_COPY_GBS), ("spec_peak", HBM_PEAK_GBS))}
+    roof_gemm = {"kernel": f"corr_pyramid_{kname} (MFMA GEMM + fused pooled-pyramid epilogue)",
+                 "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": gt,
+                 "traffic_read": tr("gemm", "read"), "traffic_write": tr("gemm", "write"),
+                 "traffic_over_algorithmic": gt / gemm_bytes if gt else None, "traffic_source": traffic_note,
+                 "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
+                 "event_samples": n_gemm,
+                 "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[mfma_dt],
+                 "mfma_frac": gemm_tfs * mfma_mult / MFMA_PEAK[mfma_dt], "mfma_products_per_flop": mfma_mult,
+                 "mfma_ceiling_at_hbm": ceil["copy_rate"], "mfma_ceiling_at_hbm_spec": ceil["spec_peak"],
+                 "mfma_ceiling_note": (f"algorithmic bytes at the {HBM_COPY_GBS / 1e3:.2f} TB/s measured copy rate "
+                                       f"(spec {HBM_PEAK_GBS / 1e3:.0f} TB/s) cap the fused-pyramid GEMM's MFMA fraction"),
+                 "algorithmic_flop_per_launch": gemm_flop}
+    roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS, "traffic": lt,
+                 "traffic_read": tr("lookup", "read"), "traffic_write": tr("lookup", "write"),
+                 "traffic_over_algorithmic": lt / look_bytes if lt else None, "traffic_source": traffic_note,
+                 "algorithmic_bytes_per_launch": look_bytes, "avg_launch_ms": look_ms,
+                 "launches_per_step": args.iters, "event_samples": n_look}
+    return roof_gemm, roof_look
+
+
+def event_ms(evs):
+    return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+
+def main():
+    args = parse()
+    maybe_launch(args)
+    world, rank, device = init_distributed(args)
+    H, W = padded(args.height, args.width)
+    h8, w8 = H // 8, W // 8
+    if args.global_batch:
+        if args.global_batch % world:
+            raise SystemExit(f"bench.py: --global-batch {args.global_batch} is not a multiple of {world} ranks")
+        args.batch = args.global_batch // world
+    B = args.batch
+
+    inputs = None if args.dry_run else rank_inputs(args, rank, world, h8, w8, device)
+    elapsed, ev_gemm, ev_look = corr_leg(args, args.precision, inputs, world, device, args.steps, args.warmup)
 
     s = 2 if args.precision in ("bf16", "fp32-f16") else 4
     compute_dt = "fp32" if args.precision.startswith("fp32") else "bf16"
@@ -537,7 +738,7 @@ def main():
         "dtype": compute_dt,
         "data": "synthetic (seeded random 1/8-res feature maps + smooth moving flow; no dataset)",
         "config": {"workload": "RAFT all-pairs correlation + 4-level pyramid + 12 radius-4 lookups "
-                               "(BASELINE configs[1])",
+                               "(BASELINE configs[1]); the whole network is the 'model_level' key",
                    "image": f"{args.height}x{args.width} padded {H}x{W}", "feature_map": f"{h8}x{w8}",
                    "channels": args.channels, "batch_per_gpu": B, "global_batch": B * world,
                    "lookups_per_step": args.iters, "precision": args.precision,
@@ -545,59 +746,45 @@ def main():
     }
     if args.dry_run:
         res["dry_run"] = "launcher / collective plumbing only: no GPU work, value meaningless"
+        if args.model_level == "on":
+            res["model_level"] = model_leg(args, world, rank, device)
     else:
-        gemm_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_gemm]))
-        look_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_look])) / args.iters
-        levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
-        # algorithmic bytes
-        look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
-        op_bytes = 2 if args.precision.startswith("bf16") else 4
-        gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
-        gemm_flop = 2.0 * B * N * N * args.channels
-        # MFMA work actually issued: the fp32 mode runs three bf16 products per k-step (x3 kernel)
-        mfma_dt, mfma_mult = ("bf16", 3.0) if args.precision == "fp32" else (compute_dt, 1.0)
-        look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
-        gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
-        gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
-        pmc = {}
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_r02.json")
-        if not os.path.exists(pmc_path):
-            pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-        if os.path.exists(pmc_path):
-            try:
-                with open(pmc_path) as fh:
-                    pmc = json.load(fh).get(args.precision, {})
-            except (OSError, ValueError):
-                pmc = {}
-        from rmd import _lib
-        kname = _lib.lib().rmd_corr_gemm_kernel(_lib.describe(B, h8, w8, args.levels, ops.PRECISIONS[args.precision][1]),
-                                                 args.channels, ops.PRECISIONS[args.precision][0])
-        roof_gemm = {"kernel": f"corr_pyramid_{kname.decode()} (MFMA GEMM + fused pooled-pyramid epilogue)",
-                     "bound": "hbm", "achieved": gemm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gemm_gbs / HBM_PEAK_GBS, "traffic": pmc.get("gemm_hbm_bytes_per_launch"),
-                     "algorithmic_bytes_per_launch": gemm_bytes, "avg_launch_ms": gemm_ms, "launches_per_step": 1,
-                     "event_samples": len(ev_gemm),
-                     "mfma_tflops": gemm_tfs, "mfma_peak_tflops": MFMA_PEAK[mfma_dt],
-                     "mfma_frac": gemm_tfs * mfma_mult / MFMA_PEAK[mfma_dt], "mfma_products_per_flop": mfma_mult,
-                     "algorithmic_flop_per_launch": gemm_flop}
-        roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS,
-                     "traffic": pmc.get("lookup_hbm_bytes_per_launch"),
-                     "algorithmic_bytes_per_launch": look_bytes, "avg_launch_ms": look_ms,
-                     "launches_per_step": args.iters, "event_samples": len(ev_look)}
-        dominant_gemm = gemm_ms >= look_ms * args.iters
+        live = rank == 0 and world == 1 and args.live_pmc == "on"
+        traffic, note = live_traffic(args, args.precision, B, rank) if live else (None, "")
+        if traffic is None:
+            fallback, fnote = stored_traffic(args.precision)
+            traffic, note = fallback, (f"{note}; " if note else "") + fnote
+        roof_gemm, roof_look = rooflines(args, args.precision, B, h8, w8, event_ms(ev_gemm),
+                                         event_ms(ev_look) / args.iters, traffic, note, len(ev_gemm), len(ev_look))
+        dominant_gemm = roof_gemm["avg_launch_ms"] >= roof_look["avg_launch_ms"] * args.iters
         res["roofline"] = roof_gemm if dominant_gemm else roof_look
         res["roofline_gemm"] = roof_gemm
         res["roofline_lookup"] = roof_look
         progress(rank, "headline leg done")
-        if rank == 0 and (args.model_level == "on" or (args.model_level == "auto" and world == 1)):
-            progress(rank, "model_level leg")
-            res["model_level"] = model_level(device, args.precision)
+        if args.fp32_mode == "on" and args.precision != "fp32":
+            # the parity mode (north_star's fp32 gate) on the same inputs: x3 GEMM + fp32 pyramid
+            progress(rank, "fp32_mode leg")
+            el32, eg32, el32l = corr_leg(args, "fp32", inputs, world, device, args.fp32_steps, 3)
+            tr32, n32 = live_traffic(args, "fp32", B, rank) if live else (None, "")
+            if tr32 is None:
+                fb, fn = stored_traffic("fp32")
+                tr32, n32 = fb, (f"{n32}; " if n32 else "") + fn
+            g32, l32 = rooflines(args, "fp32", B, h8, w8, event_ms(eg32), event_ms(el32l) / args.iters, tr32, n32,
+                                 len(eg32), len(el32l))
+            if rank == 0:
+                res["fp32_mode"] = {"value": world * B * args.fp32_steps / el32, "unit": "frame-pairs/s",
+                                    "ms_per_step": el32 / args.fp32_steps * 1e3, "steps": args.fp32_steps,
+                                    "warmup": 3, "precision": "fp32", "dtype": "fp32",
+                                    "pyramid_storage": "fp32",
+                                    "gemm": "split-bf16 x3 MFMA (hi.hi + hi.lo + lo.hi), fp32 accumulate",
+                                    "roofline_gemm": g32, "roofline_lookup": l32}
+        del inputs
+        torch.cuda.empty_cache()
         # extra legs run on every rank (batch shards / DDP collectives); a Python-level failure in one
         # (raised symmetrically on every rank, e.g. out of memory) is recorded instead of losing the
         # headline line
-        for flag, key, leg in ((args.dicl, "dicl_matching", dicl_leg), (args.hybrid, "hybrid_inference", hybrid_leg),
-                               (args.train, "train_step", train_leg)):
+        for flag, key, leg in ((args.model_level, "model_level", model_leg), (args.dicl, "dicl_matching", dicl_leg),
+                               (args.hybrid, "hybrid_inference", hybrid_leg), (args.train, "train_step", train_leg)):
             if flag != "on":
                 continue
             progress(rank, f"{key} leg")

@@ -147,8 +147,8 @@ def test_bench_launches_its_own_ranks(world):
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("WORLD_SIZE", None)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dry-run",
-                          "--backend", "gloo", "--no-cpu-baseline", "--steps", "2", "--warmup", "1"],
-                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+                          "--backend", "gloo", "--no-cpu-baseline", "--steps", "2", "--warmup", "1",
+                          "--model-level", "off"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout                      # rank 0 alone prints the JSON line
@@ -165,12 +165,38 @@ def test_bench_strong_scaling_split():
     env.pop("WORLD_SIZE", None)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
                           "--backend", "gloo", "--no-cpu-baseline", "--steps", "2", "--warmup", "1",
-                          "--global-batch", "8"], capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+                          "--global-batch", "8", "--model-level", "off"], capture_output=True, text=True, timeout=300,
+                         env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
     assert res["scaling"] == "strong" and res["config"]["global_batch"] == 8
     assert res["config"]["batch_per_gpu"] == 4
     assert abs(res["value"] - 8 * 2 / (res["ms_per_step"] * 2 / 1e3)) < 1e-6 * res["value"]
+
+
+@pytest.mark.parametrize("gb", [0, 4])
+def test_bench_model_level_leg_is_batch_sharded(gb):
+    """The whole-network leg (BASELINE.md's frame-pairs/s of the cfg2 model at 1/2/4/8 GPUs) runs on
+    EVERY rank with its own batch shard and reports the job time MAX over ranks: 2 gloo ranks, weak
+    (8 pairs per rank) and strong (--global-batch 4 -> 2 per rank).  --dry-run runs a small frame through
+    the eager correlation on the CPU: the plumbing, not the kernels."""
+    import json
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--backend", "gloo",
+           "--no-cpu-baseline", "--steps", "1", "--warmup", "0"] + (["--global-batch", str(gb)] if gb else [])
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    ml = res["model_level"]
+    per = gb // 2 if gb else 8
+    assert ml["n_gpus"] == 2 and ml["per_gpu_batch"] == per and ml["global_batch"] == 2 * per
+    assert ml["scaling"] == ("strong" if gb else "weak")
+    assert abs(ml["frame_pairs_per_s"] - 2 * per / (ml["ms_per_batch"] / 1e3)) < 1e-6 * ml["frame_pairs_per_s"]
+    assert np.isfinite(ml["rank0_flow_checksum"])
+    # both ranks reached the leg (progress lines on stderr)
+    assert "rank 0" in out.stderr and "rank 1" in out.stderr and "model_level" in out.stderr
 
 
 def test_bench_rejects_world_size_mismatch():
