@@ -133,6 +133,31 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
                         int compute, const float* coords, int radius, unsigned zero_level_mask, float* out,
                         void* stream);
 
+/*
+ * Backward of the on-the-fly lookup (training at resolutions where the volume does not fit; autograd of
+ * raft_fs.py:25-87 — grid_sample backward, the matmul with fmap1 and the avg-pool chain — without any
+ * O(N^2) buffer).  After each lookup's forward, its backward records the lookup's per-query patch
+ * weights: rmd_corr_otf_record turns grad_out (B, L*(2r+1)^2, H, W) and the lookup's coords into a
+ * record of rmd_corr_otf_record_bytes() (per level and query: the window origin and the (2r+2)^2
+ * bilinear patch weights of grad_out).  rmd_corr_otf_backward then computes, from all records of one
+ * rmd_corr_otf_prepare (fmap1, fmap2, scale as given there, its workspace unchanged):
+ *   grad_fmap1 = scale * sum_l G_l P_l,   grad_fmap2 = sum_l avgpool_l^T(G_l^T (scale * fmap1))
+ * with G_l the sum of the records' level-l patch weights and P_l the level-l pooled fmap2; both
+ * outputs are overwritten (B, C, H, W) float32.  C <= 256.  compute as in rmd_corr_otf_prepare
+ * (RMD_F32 and RMD_BF16X3: split-bf16 products, fp32 accumulation; RMD_BF16: bf16 products).
+ * Masked and 1-pixel levels and non-finite coordinates record no contribution.  `records` is a host
+ * array of `nrecords` device pointers.  Not deterministic (float atomics into the pooled gradient,
+ * like ATen's grid_sampler_2d_backward).
+ */
+size_t rmd_corr_otf_record_bytes(int batch, int height, int width, int levels, int radius);
+int rmd_corr_otf_record(const float* grad_out, const float* coords, int batch, int height, int width, int levels,
+                        int radius, unsigned zero_level_mask, void* record, void* stream);
+size_t rmd_corr_otf_backward_workspace_bytes(int batch, int channels, int height, int width, int levels, int compute);
+int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, const void* otf_workspace, int batch, int channels,
+                          int height, int width, int levels, float scale, int compute, int radius, int nrecords,
+                          const void* const* records, float* grad_fmap1, float* grad_fmap2, void* workspace,
+                          void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Backward of the RAFT correlation (training; autograd of raft.py:18-95).  Coordinates are
  * detached in the reference (raft.py:402), so only the feature maps receive gradients.

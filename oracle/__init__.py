@@ -10,7 +10,7 @@ product path (``raft-meets-dicl_amd/``) never imports it and has no CPU fallback
 """
 
 from .corr import (corr_volume, corr_pyramid, corr_lookup, corr_lookup_fs, corr_lookup_backward,
-                   pyramid_level_shapes)
+                   corr_lookup_fs_backward, pyramid_level_shapes)
 from .dicl import (dicl_stack, dicl_stack_at, dicl_stack_backward, dicl_stack_int, dicl_stack_int_at,
                    dicl_stack_int_backward, dap, dap_backward,
                    warp_backwards, warp_backwards_backward)
@@ -18,6 +18,7 @@ from .heads import up8, up8_backward, softargmax, softargmax_backward
 from .input import input_images, input_flow, pad_extents
 
 __all__ = ["corr_volume", "corr_pyramid", "corr_lookup", "corr_lookup_fs", "corr_lookup_backward",
+           "corr_lookup_fs_backward",
            "pyramid_level_shapes", "dicl_stack", "dicl_stack_at", "dicl_stack_backward", "dicl_stack_int",
            "dicl_stack_int_at",
            "dicl_stack_int_backward", "dap", "dap_backward", "up8", "up8_backward", "softargmax",

@@ -240,3 +240,17 @@ def corr_lookup_backward(fmap1, fmap2, coords, levels, radius, grad_out, mask_co
     gf1 = np.matmul(f2, gcorr0.transpose(0, 2, 1)).reshape(b, c, h, w)
     gf2 = np.matmul(f1, gcorr0).reshape(b, c, h, w)
     return gf1, gf2
+
+
+def corr_lookup_fs_backward(fmap1, fmap2, coords, levels, radius, grad_out, mask_costs=(), scale=None):
+    """d(sum(out*grad_out))/d(fmap1, fmap2) for raft_fs.CorrBlock (raft_fs.py:13-87; autograd of its
+    avg_pool2d chain, grid_sample and matmul), with corr_lookup_fs's ``scale`` (None -> 1).
+
+    raft_fs's output equals raft.CorrBlock's times sqrt(C) (pooling fmap2
+    commutes with the product), so its gradient is corr_lookup_backward's times sqrt(C) * scale.
+    """
+    c = fmap1.shape[1]
+    k = np.sqrt(np.asarray(c, dtype=fmap1.dtype)) * np.asarray(1.0 if scale is None else scale, dtype=fmap1.dtype)
+    g1, g2 = corr_lookup_backward(fmap1, fmap2, coords, levels, radius, grad_out, mask_costs)
+    return g1 * k, g2 * k
+

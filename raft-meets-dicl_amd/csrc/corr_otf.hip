@@ -28,6 +28,8 @@
 // takes a per-query VALU patch path.
 #include "rmd_common.h"
 
+#include <algorithm>
+
 namespace rmd {
 namespace {
 
@@ -133,6 +135,10 @@ otf_pool2_kernel(const float* __restrict__ src, int BC, int h, int w, float* __r
 
 struct LevelSrc {
     const float* p[RMD_MAX_LEVELS];      // (B, C, lh, lw) float32 per level
+};
+
+struct LevelOff {
+    long long o[RMD_MAX_LEVELS];
 };
 
 // Segment operands: one thread per 16-B lane chunk (segment, load step, lane); a wave writes one
@@ -451,6 +457,332 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward (training).  With G_l the gradient of the level-l window products w.r.t. the pooled targets
+// (per query the (2r+2)^2 bilinear patch weights of its grad_out window, raft_fs.py:68-74 transposed),
+//   d q~ = sum_l G_l . P_l      (q~ = fmap1 * scale, the query operand)
+//   d P_l = G_l^T . q~          (P_l the level-l pooled fmap2, raft_fs.py:25-31)
+// and d fmap2 = sum_l avgpool_l^T(d P_l).  Coordinates carry no gradient (raft.py:402).
+//
+// Every lookup of a block records its patch weights (otf_record_kernel: origin + K*K weights per
+// (level, query), no volume); one launch after the last lookup backward turns all records into the
+// two products, so the box of target rows a query tile touches is swept once for all iterations:
+//  * one 512-thread workgroup per 32 x 4 query tile; per level the union box of the tile's patches
+//    over all records, swept in bands of one target row x kBwdTB columns;
+//  * per band the dense G (128 queries x kBwdTB targets, fp32) is summed into LDS from the records
+//    (LDS float atomics: a query's patches of several iterations overlap);
+//  * d q~ (128 queries x C) += G . P_band: v_mfma_f32_32x32x16_bf16 with A = G rows from LDS and B =
+//    the band's targets in the "T layout" (lane c + 32h holds pixels 8h..8h+7 of channel c of a 16-pixel
+//    segment: the B fragment of a 16-target k-step), accumulated in registers over all bands;
+//  * d P_band (kBwdTB targets x C) = G^T . q~: A = G columns from LDS, B = the tile's queries in the T
+//    layout; the 32 x 32 result tiles go to a pixel-major fp32 d P with float atomics (two 128-B
+//    segments per instruction: the full-rate shape, MI355X_MICROARCH.md §Global float atomics).
+// fp32 modes split G and both operands into bf16 hi + lo and accumulate lo.hi + hi.lo + hi.hi (the
+// forward x3 split); bf16 mode uses one product.
+constexpr int kBwdQX = 32, kBwdQY = 4, kBwdQ = kBwdQX * kBwdQY;
+constexpr int kBwdTB = 128;                          // band width (targets)
+constexpr int kBwdLd = kBwdTB + 4;                   // G row stride (floats): conflict-free row and column reads
+constexpr int kBwdThreads = 512;
+constexpr int kMaxRec = 32;                          // records per launch (more: several launches)
+constexpr int kFar = -(1 << 29);                     // origin of a masked / degenerate level
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+struct OtfRecords {
+    const int2* org[kMaxRec];                       // (L, B, N) patch origins (x0, y0) at level l
+    const float* wp[kMaxRec];                       // (L, B, K*K, N) patch weights
+    int n;
+};
+
+size_t otf_record_org_bytes(int B, int H, int W, int L) {
+    return ((size_t)L * B * H * W * sizeof(int2) + 255) / 256 * 256;
+}
+
+// per (level, batch, query): origin and the (2r+2)^2 patch weights of grad_out's window
+//   wp[j][k] = (1-fy) hx(k, j) + fy hx(k, j-1),  hx(k, bb) = (1-fx) g[k][bb] + fx g[k-1][bb]
+// (g[a][bb] = grad_out channel l*D*D + a*D + bb; out-of-range a / bb -> 0).  Masked and 1-pixel levels
+// record kFar (no contribution); a non-finite coordinate clamps far off the map (no contribution).
+template <int R>
+__global__ void __launch_bounds__(kThreads)
+otf_record_kernel(const float* __restrict__ gout, const float* __restrict__ coords, OtfGeom g, unsigned zmask,
+                  int2* __restrict__ org, float* __restrict__ wp) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    const long long N = (long long)g.H * g.W;
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= (long long)g.L * g.B * N) return;
+    const int q = (int)(idx % N);
+    const int b = (int)((idx / N) % g.B);
+    const int l = (int)(idx / (N * g.B));
+    const int lh = g.lh[l], lw = g.lw[l];
+    const float x = coords[((size_t)b * 2 + 0) * N + q], y = coords[((size_t)b * 2 + 1) * N + q];
+    const float inv = 1.0f / (float)(1 << l);
+    const float rx = x * inv, ry = y * inv;
+    const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f), cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
+    const bool dead = ((zmask >> l) & 1u) || lh < 2 || lw < 2 || !(rx == rx) || !(ry == ry);
+    org[idx] = dead ? make_int2(kFar, kFar) : make_int2((int)floorf(cx) - R, (int)floorf(cy) - R);
+    const float fx = rx - floorf(rx), fy = ry - floorf(ry);
+    const float* gp = gout + ((size_t)b * g.L + l) * D * D * N + q;
+    float gv[D][D];
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+        for (int bb = 0; bb < D; ++bb) gv[a][bb] = dead ? 0.f : gp[(size_t)(a * D + bb) * N];
+    float* w = wp + ((size_t)l * g.B + b) * K * K * N + q;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            auto hx = [&](int bb) {
+                if (bb < 0 || bb >= D) return 0.f;
+                const float v0 = k < D ? gv[k][bb] : 0.f, v1 = k >= 1 ? gv[k - 1][bb] : 0.f;
+                return (1.f - fx) * v0 + fx * v1;
+            };
+            const float v = (1.f - fy) * hx(j) + fy * hx(j - 1);
+            w[(size_t)(j * K + k) * N] = dead ? 0.f : v;
+        }
+    }
+}
+
+// T layout of a planar (B, C, h, w) fp32 map (times s): unit (b, level segment row/seg, channel group cg)
+// = 64 lanes x 8 elements, lane c + 32h = pixels 8h..8h+7 of channel 32cg + c (zero past the map / C);
+// X3: the unit's lo half follows its hi half.  One thread per (unit, lane).
+template <bool X3>
+__global__ void __launch_bounds__(kThreads)
+otf_tlayout_kernel(LevelSrc src, OtfGeom g, float s, __bf16* __restrict__ dst) {
+    constexpr int NP = X3 ? 2 : 1;
+    const int ncg = g.Cp / 32;
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= (long long)g.B * g.TS * ncg * 64) return;
+    const int lane = (int)(idx & 63), c32 = lane & 31, h = lane >> 5;
+    const long long u = idx >> 6;
+    const int cg = (int)(u % ncg);
+    const long long bs = u / ncg;
+    const long long sg = bs % g.TS;
+    const int b = (int)(bs / g.TS);
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < RMD_MAX_LEVELS; ++k)
+        if (k < g.L && sg >= g.soff[k]) l = k;
+    const int sl = (int)(sg - g.soff[l]);
+    const int y = sl / g.nsx[l], x0 = (sl - y * g.nsx[l]) * 16 + 8 * h;
+    const int c = 32 * cg + c32;
+    const size_t plane = (size_t)g.lh[l] * g.lw[l];
+    const float* row = src.p[l] + ((size_t)b * g.C + (c < g.C ? c : 0)) * plane + (size_t)y * g.lw[l];
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float v = (c < g.C && x0 + e < g.lw[l]) ? row[x0 + e] * s : 0.f;
+        hi[e] = (__bf16)v;
+        lo[e] = (__bf16)(v - (float)hi[e]);
+    }
+    __bf16* o = dst + ((size_t)u * NP * 64 + lane) * 8;
+    *reinterpret_cast<bf16x8*>(o) = hi;
+    if constexpr (X3) *reinterpret_cast<bf16x8*>(o + 64 * 8) = lo;
+}
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        hi[e] = (__bf16)v[e];
+        lo[e] = (__bf16)(v[e] - (float)hi[e]);
+    }
+}
+
+template <bool X3>
+__device__ __forceinline__ void mma3(f32x16& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                     const bf16x8& bl) {
+    if constexpr (X3) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+struct BwdArgs {
+    OtfGeom g;                  // targets (all levels); g.QS / g.qnsx: query segments
+    const __bf16* pt;           // targets, T layout (B, TS, ncg units)
+    const __bf16* qt;           // queries (fmap1 * scale), T layout (B, QS, ncg units)
+    OtfRecords rec;
+    float* dP;                  // (B, PT, C) pixel-major fp32, += G^T q~
+    long long pT;               // pooled pixels per batch (all levels)
+    long long poff[RMD_MAX_LEVELS];
+    float* gq;                  // (B, C, H, W) fp32, += scale * G P
+    float scale;
+};
+
+template <bool X3, int R>
+__global__ void __launch_bounds__(kBwdThreads, 1)
+otf_backward_kernel(BwdArgs a) {
+    constexpr int K = 2 * R + 2;
+    constexpr int NP = X3 ? 2 : 1;
+    extern __shared__ float G[];                                     // [kBwdQ][kBwdLd]
+    __shared__ int2 sorg[kMaxRec][kBwdQ];
+    __shared__ int box[4];
+    const OtfGeom& g = a.g;
+    const int N = g.H * g.W;
+    const int nbx = (g.W + kBwdQX - 1) / kBwdQX, nqb = nbx * ((g.H + kBwdQY - 1) / kBwdQY);
+    const int lid = xcd_block(blockIdx.x, gridDim.x);
+    const int qb = lid % nqb, b = lid / nqb;
+    const int qx0 = (qb % nbx) * kBwdQX, qy0 = (qb / nbx) * kBwdQY;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int j32 = lane & 31, h = lane >> 5;
+    const int ncg = g.Cp / 32;
+    const int mt = w & 3;                                            // query row / target tile of this wave
+    const int nt0 = (w >> 2) * 4;                                    // first channel tile of this wave
+    const int ntn = max(0, min(4, ncg - nt0));
+    const size_t unit = (size_t)64 * 8 * NP;                         // elements per T-layout unit
+
+    f32x16 accq[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) accq[t] = f32x16{};
+
+    for (int l = 0; l < g.L; ++l) {
+        const int lh = g.lh[l], lw = g.lw[l];
+        // ---- origins of every record for the tile's queries, and their union box at this level ----
+        __syncthreads();                                             // previous level's G / sorg reads done
+        if (tid < 4) box[tid] = (tid & 1) ? -(1 << 30) : (1 << 30);
+        __syncthreads();
+        for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
+            const int r = i / kBwdQ, q = i % kBwdQ;
+            const int y = qy0 + q / kBwdQX, x = qx0 + q % kBwdQX;
+            int2 o = make_int2(kFar, kFar);
+            if (y < g.H && x < g.W) o = a.rec.org[r][((size_t)l * g.B + b) * N + y * g.W + x];
+            // patches entirely off the map contribute nothing
+            if (o.x + K - 1 < 0 || o.x >= lw || o.y + K - 1 < 0 || o.y >= lh) o = make_int2(kFar, kFar);
+            sorg[r][q] = o;
+            if (o.x != kFar) {
+                atomicMin(&box[0], max(o.x, 0));
+                atomicMax(&box[1], min(o.x + K - 1, lw - 1));
+                atomicMin(&box[2], max(o.y, 0));
+                atomicMax(&box[3], min(o.y + K - 1, lh - 1));
+            }
+        }
+        __syncthreads();
+        const int bx0 = box[0], bx1 = box[1], by0 = box[2], by1 = box[3];
+        if (bx0 > bx1) continue;                                     // uniform: nothing at this level
+        const __bf16* plev = a.pt + ((size_t)b * g.TS + g.soff[l]) * ncg * unit;
+        for (int ty = by0; ty <= by1; ++ty) {
+            for (int cx = bx0 & ~15; cx <= bx1; cx += kBwdTB) {
+                const int ncols = min(kBwdTB, ((bx1 - cx + 1) + 15) & ~15);
+                // ---- G (queries x band targets) from every record's patch row ty ----------------------
+                __syncthreads();                                     // previous band's G reads done
+                for (int i = tid; i < kBwdQ * kBwdLd; i += kBwdThreads) G[i] = 0.f;
+                __syncthreads();
+                for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
+                    const int r = i / kBwdQ, q = i % kBwdQ;
+                    const int2 o = sorg[r][q];
+                    const int j = ty - o.y;
+                    if (o.x == kFar || j < 0 || j >= K || o.x + K <= cx || o.x >= cx + ncols) continue;
+                    const int y = qy0 + q / kBwdQX, x = qx0 + q % kBwdQX;
+                    const float* wr = a.rec.wp[r] + (((size_t)l * g.B + b) * K * K + j * K) * N + y * g.W + x;
+                    float* grow = G + q * kBwdLd;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int col = o.x + k - cx, tx = o.x + k;
+                        if (col >= 0 && col < ncols && tx >= 0 && tx < lw) atomicAdd(grow + col, wr[(size_t)k * N]);
+                    }
+                }
+                __syncthreads();
+                // ---- d q~ += G . P_band (query tile mt, channel tiles nt0..nt0+ntn-1) ------------------
+                for (int ks = 0; ks < ncols / 16; ++ks) {
+                    const float* gr = G + (mt * 32 + j32) * kBwdLd + ks * 16 + 8 * h;
+                    float v[8];
+                    *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(gr);
+                    *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(gr + 4);
+                    bf16x8 ah, al;
+                    split8(v, ah, al);
+                    const __bf16* pu = plev + ((size_t)(ty * g.nsx[l] + (cx >> 4) + ks) * ncg) * unit + lane * 8;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (t >= ntn) break;
+                        const __bf16* pp = pu + (size_t)(nt0 + t) * unit;
+                        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pp);
+                        const bf16x8 bl = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh;
+                        mma3<X3>(accq[t], ah, al, bh, bl);
+                    }
+                }
+                // ---- d P_band = G^T . q~ (target tile mt, channel tiles nt0..), float atomics ------------
+                if (mt * 32 < ncols && ntn > 0) {
+                    f32x16 accp[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) accp[t] = f32x16{};
+                    for (int ks = 0; ks < kBwdQ / 16; ++ks) {
+                        const int qrow = qy0 + (ks >> 1);
+                        if (qrow >= g.H) break;                      // uniform
+                        float v[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] = G[(ks * 16 + 8 * h + e) * kBwdLd + mt * 32 + j32];
+                        bf16x8 ah, al;
+                        split8(v, ah, al);
+                        const int qsx = (qx0 >> 4) + (ks & 1);
+                        if (qsx >= g.qnsx) continue;                 // uniform: a segment past the map's width
+                        const __bf16* qu = a.qt + ((size_t)(b * g.QS + qrow * g.qnsx + qsx) * ncg) * unit + lane * 8;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            if (t >= ntn) break;
+                            const __bf16* pp = qu + (size_t)(nt0 + t) * unit;
+                            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pp);
+                            const bf16x8 bl = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh;
+                            mma3<X3>(accp[t], ah, al, bh, bl);
+                        }
+                    }
+                    // lane (channel j32, half h): register 4i + k is target column mt*32 + 8i + 4h + k
+                    float* drow = a.dP + ((size_t)b * a.pT + a.poff[l] + (size_t)ty * lw) * g.C;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (t >= ntn) break;
+                        const int ch = (nt0 + t) * 32 + j32;
+#pragma unroll
+                        for (int v = 0; v < 16; ++v) {
+                            const int col = mt * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+                            const int tx = cx + col;
+                            if (col < ncols && tx <= bx1 && ch < g.C) atomicAdd(drow + (size_t)tx * g.C + ch, accp[t][v]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // ---- d fmap1 (planar) += scale * d q~: lane (channel j32, half h), register 4i + k = query x 8i+4h+k ----
+    const int y = qy0 + mt;
+    if (y < g.H) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (t >= ntn) break;
+            const int ch = (nt0 + t) * 32 + j32;
+            if (ch >= g.C) continue;
+            float* o = a.gq + ((size_t)b * g.C + ch) * N + (size_t)y * g.W + qx0;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int x = 8 * (v >> 2) + 4 * h + (v & 3);
+                if (qx0 + x < g.W) o[x] += a.scale * accq[t][v];
+            }
+        }
+    }
+}
+
+// d fmap2[b, c, y, x] = sum_l d P_l[b, (y >> l, x >> l), c] / 4^l over the floor-cropped part of each level
+// (the transpose of l successive 2x2 average pools); one thread per (b, y, x, c), channel fastest.
+__global__ void __launch_bounds__(kThreads)
+otf_unpool_kernel(const float* __restrict__ dP, OtfGeom g, long long pT, LevelOff po, float* __restrict__ gf2) {
+    const long long N = (long long)g.H * g.W;
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= (long long)g.B * N * g.C) return;
+    const int c = (int)(idx % g.C);
+    const long long p = (idx / g.C) % N;
+    const int b = (int)(idx / ((long long)g.C * N));
+    const int y = (int)(p / g.W), x = (int)(p % g.W);
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
+        if (l >= g.L) break;
+        const int yy = y >> l, xx = x >> l;
+        if (yy < g.lh[l] && xx < g.lw[l])
+            s += dP[((size_t)b * pT + po.o[l] + (size_t)yy * g.lw[l] + xx) * g.C + c] * (1.0f / (float)(1 << (2 * l)));
+    }
+    gf2[((size_t)b * g.C + c) * N + p] = s;
+}
+
 int check_otf(int batch, int channels, int height, int width, int levels, int compute) {
     RMD_REQUIRE(batch > 0 && channels > 0 && height > 0 && width > 0, RMD_ERR_SHAPE, "rmd_corr_otf: bad sizes");
     RMD_REQUIRE(levels >= 1 && levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_otf: bad levels");
@@ -590,4 +922,171 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #undef RMD_OTF
 #undef RMD_OTF_K
     return check_launch("rmd_corr_otf_lookup");
+}
+
+// ---- backward entry points -------------------------------------------------------------------------
+
+namespace {
+
+struct BwdLayout {
+    OtfGeom g, gq;              // targets (all levels) / queries (level 0 of fmap1)
+    size_t pt_off, qt_off, dp_off, total;
+    long long pT;
+    long long poff[RMD_MAX_LEVELS];
+};
+
+BwdLayout bwd_layout(int B, int C, int H, int W, int L, int compute) {
+    BwdLayout y{};
+    y.g = make_otf_geom(B, C, H, W, L);
+    y.gq = make_otf_geom(B, C, H, W, 1);
+    y.g.Cp = y.gq.Cp = (C + 31) / 32 * 32;                // T layout: 32-channel groups
+    y.g.QS = y.gq.TS;
+    y.g.qnsx = y.gq.nsx[0];
+    const size_t np = compute == RMD_BF16 ? 1 : 2;
+    const size_t ncg = (size_t)y.g.Cp / 32;
+    const size_t tbytes = (size_t)B * y.g.TS * ncg * 512 * np * 2, qbytes = (size_t)B * y.gq.TS * ncg * 512 * np * 2;
+    long long p = 0;
+    for (int l = 0; l < L; ++l) {
+        y.poff[l] = p;
+        p += (long long)y.g.lh[l] * y.g.lw[l];
+    }
+    y.pT = p;
+    y.pt_off = 0;
+    y.qt_off = (tbytes + 255) / 256 * 256;
+    y.dp_off = y.qt_off + (qbytes + 255) / 256 * 256;
+    y.total = y.dp_off + (size_t)B * p * C * sizeof(float);
+    return y;
+}
+
+}  // namespace
+
+extern "C" size_t rmd_corr_otf_record_bytes(int batch, int height, int width, int levels, int radius) {
+    if (batch <= 0 || height <= 0 || width <= 0 || levels < 1 || levels > RMD_MAX_LEVELS || radius < 1 || radius > 8)
+        return 0;
+    const size_t K = 2 * radius + 2;
+    return otf_record_org_bytes(batch, height, width, levels) + (size_t)levels * batch * height * width * K * K * sizeof(float);
+}
+
+extern "C" int rmd_corr_otf_record(const float* grad_out, const float* coords, int batch, int height, int width,
+                                   int levels, int radius, unsigned zero_level_mask, void* record, void* stream) {
+    RMD_REQUIRE(grad_out && coords && record, RMD_ERR_ARG, "rmd_corr_otf_record: null pointer");
+    RMD_REQUIRE(rmd_corr_otf_record_bytes(batch, height, width, levels, radius) > 0, RMD_ERR_SHAPE,
+                "rmd_corr_otf_record: bad sizes or radius %d not in 1..8", radius);
+    const OtfGeom g = make_otf_geom(batch, 1, height, width, levels);
+    int2* org = static_cast<int2*>(record);
+    float* wp = reinterpret_cast<float*>(static_cast<char*>(record) + otf_record_org_bytes(batch, height, width, levels));
+    const long long n = (long long)levels * batch * height * width;
+    const unsigned blocks = (unsigned)((n + kThreads - 1) / kThreads);
+    hipStream_t st = as_stream(stream);
+    switch (radius) {
+#define RMD_CASE(RR) case RR: otf_record_kernel<RR><<<blocks, kThreads, 0, st>>>(grad_out, coords, g, zero_level_mask, org, wp); break;
+        RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
+#undef RMD_CASE
+    }
+    return check_launch("rmd_corr_otf_record");
+}
+
+extern "C" size_t rmd_corr_otf_backward_workspace_bytes(int batch, int channels, int height, int width, int levels,
+                                                        int compute) {
+    if (check_otf(batch, channels, height, width, levels, compute) || channels > 256) return 0;
+    return bwd_layout(batch, channels, height, width, levels, compute).total;
+}
+
+extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, const void* otf_workspace, int batch,
+                                     int channels, int height, int width, int levels, float scale, int compute,
+                                     int radius, int nrecords, const void* const* records, float* grad_fmap1,
+                                     float* grad_fmap2, void* workspace, void* stream) {
+    RMD_REQUIRE(fmap1 && fmap2 && otf_workspace && grad_fmap1 && grad_fmap2 && workspace && (records || nrecords == 0),
+                RMD_ERR_ARG, "rmd_corr_otf_backward: null pointer");
+    int rc = check_otf(batch, channels, height, width, levels, compute);
+    if (rc) return rc;
+    RMD_REQUIRE(channels <= 256, RMD_ERR_SHAPE, "rmd_corr_otf_backward: channels %d > 256", channels);
+    RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_otf_backward: radius %d not in 1..8", radius);
+    hipStream_t st = as_stream(stream);
+    const BwdLayout y = bwd_layout(batch, channels, height, width, levels, compute);
+    const bool x3 = compute != RMD_BF16;
+    char* ws = static_cast<char*>(workspace);
+    __bf16* pt = reinterpret_cast<__bf16*>(ws + y.pt_off);
+    __bf16* qt = reinterpret_cast<__bf16*>(ws + y.qt_off);
+    float* dP = reinterpret_cast<float*>(ws + y.dp_off);
+    const size_t N = (size_t)height * width;
+    if (hipMemsetAsync(grad_fmap1, 0, (size_t)batch * channels * N * sizeof(float), st) != hipSuccess ||
+        hipMemsetAsync(dP, 0, (size_t)batch * y.pT * channels * sizeof(float), st) != hipSuccess) {
+        set_error("rmd_corr_otf_backward: hipMemsetAsync failed");
+        return RMD_ERR_LAUNCH;
+    }
+    // operands in the T layout: pooled targets from the forward workspace's fp32 levels, queries = fmap1 * scale
+    {
+        const OtfGeom gf = make_otf_geom(batch, channels, height, width, levels);
+        const size_t es = compute == RMD_BF16 ? 2 : 4;
+        const float* scratch = reinterpret_cast<const float*>(static_cast<const char*>(otf_workspace) +
+                                                              otf_scratch_offset(gf, es));
+        LevelSrc lt{}, lq{};
+        lt.p[0] = fmap2;
+        for (int l = 1; l < levels; ++l) {
+            lt.p[l] = scratch;
+            scratch += (size_t)batch * channels * gf.lh[l] * gf.lw[l];
+        }
+        lq.p[0] = fmap1;
+        const long long nt = (long long)batch * y.g.TS * (y.g.Cp / 32) * 64;
+        const long long nq = (long long)batch * y.gq.TS * (y.gq.Cp / 32) * 64;
+        if (x3) {
+            otf_tlayout_kernel<true><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt);
+            otf_tlayout_kernel<true><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt);
+        } else {
+            otf_tlayout_kernel<false><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt);
+            otf_tlayout_kernel<false><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt);
+        }
+        rc = check_launch("rmd_corr_otf_backward (operands)");
+        if (rc) return rc;
+    }
+    const long long nblk = (long long)((width + kBwdQX - 1) / kBwdQX) * ((height + kBwdQY - 1) / kBwdQY) * batch;
+    RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_backward: grid too large");
+    const size_t lds = sizeof(float) * kBwdQ * kBwdLd;
+    const size_t obytes = otf_record_org_bytes(batch, height, width, levels);
+    for (int r0 = 0; r0 < nrecords; r0 += kMaxRec) {
+        BwdArgs a{};
+        a.g = y.g;
+        a.pt = pt;
+        a.qt = qt;
+        a.dP = dP;
+        a.pT = y.pT;
+        for (int l = 0; l < RMD_MAX_LEVELS; ++l) a.poff[l] = y.poff[l];
+        a.gq = grad_fmap1;
+        a.scale = scale;
+        a.rec.n = std::min(kMaxRec, nrecords - r0);
+        for (int i = 0; i < a.rec.n; ++i) {
+            RMD_REQUIRE(records[r0 + i], RMD_ERR_ARG, "rmd_corr_otf_backward: null record %d", r0 + i);
+            a.rec.org[i] = static_cast<const int2*>(records[r0 + i]);
+            a.rec.wp[i] = reinterpret_cast<const float*>(static_cast<const char*>(records[r0 + i]) + obytes);
+        }
+#define RMD_BWD(XX, RR)                                                                                          \
+        do {                                                                                                     \
+            auto k = otf_backward_kernel<XX, RR>;                                                                \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                      (int)lds);                                                                 \
+            k<<<(unsigned)nblk, kBwdThreads, lds, st>>>(a);                                                      \
+        } while (0)
+#define RMD_BWD_R(XX)                                                                                            \
+        switch (radius) {                                                                                        \
+            case 1: RMD_BWD(XX, 1); break;                                                                       \
+            case 2: RMD_BWD(XX, 2); break;                                                                       \
+            case 3: RMD_BWD(XX, 3); break;                                                                       \
+            case 4: RMD_BWD(XX, 4); break;                                                                       \
+            case 5: RMD_BWD(XX, 5); break;                                                                       \
+            case 6: RMD_BWD(XX, 6); break;                                                                       \
+            case 7: RMD_BWD(XX, 7); break;                                                                       \
+            default: RMD_BWD(XX, 8); break;                                                                      \
+        }
+        if (x3) { RMD_BWD_R(true) } else { RMD_BWD_R(false) }
+#undef RMD_BWD_R
+#undef RMD_BWD
+        rc = check_launch("rmd_corr_otf_backward");
+        if (rc) return rc;
+    }
+    LevelOff po{};
+    for (int l = 0; l < RMD_MAX_LEVELS; ++l) po.o[l] = y.poff[l];
+    const long long n2 = (long long)batch * N * channels;
+    otf_unpool_kernel<<<(unsigned)((n2 + kThreads - 1) / kThreads), kThreads, 0, st>>>(dP, y.g, y.pT, po, grad_fmap2);
+    return check_launch("rmd_corr_otf_backward (unpool)");
 }

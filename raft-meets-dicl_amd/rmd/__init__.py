@@ -14,7 +14,7 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.input.InputSpec / ModuloPadding   <- src/models/input.py:32-313 (frame pair + flow target format)
 """
 
-from . import blocks, corr, dicl, heads, input, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
+from . import blocks, config, corr, dicl, heads, input, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

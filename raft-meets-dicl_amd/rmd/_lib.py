@@ -52,6 +52,11 @@ _SIGS = {
     "rmd_corr_otf_workspace_bytes": (ctypes.c_size_t, [_I] * 6),
     "rmd_corr_otf_prepare": (_I, [_P, _P] + [_I] * 5 + [ctypes.c_float, _I, _P, _P]),
     "rmd_corr_otf_lookup": (_I, [_P] + [_I] * 6 + [_P, _I, _U, _P, _P]),
+    "rmd_corr_otf_record_bytes": (ctypes.c_size_t, [_I] * 5),
+    "rmd_corr_otf_record": (_I, [_P, _P] + [_I] * 5 + [_U, _P, _P]),
+    "rmd_corr_otf_backward_workspace_bytes": (ctypes.c_size_t, [_I] * 6),
+    "rmd_corr_otf_backward": (_I, [_P, _P, _P] + [_I] * 5 + [ctypes.c_float, _I, _I, _I, ctypes.POINTER(_P), _P, _P,
+                                                               _P, _P]),
     "rmd_corr_grad_targets": (ctypes.c_longlong, [_I, _I, _I]),
     "rmd_corr_lookup_backward": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
     "rmd_corr_pool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),

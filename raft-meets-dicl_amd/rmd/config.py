@@ -1,0 +1,114 @@
+"""Op selection from the model configuration — the drop-in's answer to SURVEY.md §5 "Config / flags".
+
+The reference builds every model from a cfg/model/*.yaml whose ``model.parameters`` section goes to
+``Model.from_config`` (e.g. src/models/impls/raft_fs.py:175-197 reads 'corr-levels', 'corr-radius',
+'mixed-precision', ... with ``param_cfg.get(key, default)``) and comes back out of ``get_config()``.
+The correlation blocks it then constructs take only ``(fmap1, fmap2, num_levels, radius)``
+(raft.py:384, raft_fs.py:132).  The drop-in reads three more keys from that same ``parameters``
+section; all are optional and their defaults reproduce the reference:
+
+  corr-precision      fp32 (default: split-bf16 MFMA, fp32 pyramid, ~1e-5 of the reference) |
+                      fp32-exact | bf16 (bf16 MFMA, fp16 pyramid: the bench mode) | bf16-f32 | fp32-f16
+  corr-method         auto (default) | volume | otf — all-pairs pyramid + lookup, or the on-the-fly
+                      lookup with no O(N^2) buffer (both differentiable); auto takes the volume unless
+                      its bytes (pyramid, plus the dense fp32 gradient when training) pass the budget
+  corr-memory-budget  bytes the volume may take before auto switches to otf (int, or a string with a
+                      KiB / MiB / GiB suffix; default 16 GiB)
+
+A maintainer passes them where the reference reads its other parameters — either per block:
+    CorrBlock(fmap1, fmap2, num_levels=..., radius=..., **rmd.config.corr_options(param_cfg).kwargs())
+or once per process, from ``Model.from_config``:  ``rmd.config.configure(cfg['parameters'])``
+(INTEGRATION.md §2).  Blocks constructed with ``precision=None`` / ``method=None`` use the process
+values.
+"""
+
+import re
+from collections import namedtuple
+
+PRECISIONS = ("fp32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16")
+METHODS = ("auto", "volume", "otf")
+KEYS = ("corr-precision", "corr-method", "corr-memory-budget")
+DEFAULTS = {"corr-precision": "fp32", "corr-method": "auto", "corr-memory-budget": 16 << 30}
+
+_STORAGE_BYTES = {"fp32": 4, "fp32-exact": 4, "bf16": 2, "bf16-f32": 4, "fp32-f16": 2}
+
+
+class CorrOptions(namedtuple("CorrOptions", ["precision", "method", "memory_budget"])):
+    """Validated correlation options (constructor keyword arguments of the drop-in blocks)."""
+
+    def kwargs(self):
+        return {"precision": self.precision, "method": self.method, "memory_budget": self.memory_budget}
+
+    def parameters(self):
+        """The ``parameters`` entries that reproduce these options (for ``Model.get_config``)."""
+        return {"corr-precision": self.precision, "corr-method": self.method,
+                "corr-memory-budget": self.memory_budget}
+
+
+def _bytes(v):
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        if v <= 0:
+            raise ValueError(f"corr-memory-budget must be positive, got {v}")
+        return int(v)
+    m = re.fullmatch(r"\s*([0-9]+(?:\.[0-9]*)?)\s*([KMGT]i?B?|B)?\s*", str(v), re.IGNORECASE)
+    if not m:
+        raise ValueError(f"corr-memory-budget: cannot parse {v!r} (bytes, or a number with KiB/MiB/GiB)")
+    unit = (m.group(2) or "B").upper().rstrip("B").rstrip("I")
+    mult = {"": 1, "K": 1 << 10, "M": 1 << 20, "G": 1 << 30, "T": 1 << 40}[unit]
+    return _bytes(float(m.group(1)) * mult)
+
+
+def corr_options(parameters=None, **overrides):
+    """CorrOptions from a cfg/model ``parameters`` mapping (missing keys: the process values), with
+    keyword overrides ``precision`` / ``method`` / ``memory_budget``.  Unknown values raise ValueError,
+    as the reference's from_config does for bad types."""
+    base = _current
+    p = dict(parameters or {})
+    precision = overrides.get("precision") or p.get("corr-precision", base.precision)
+    method = overrides.get("method") or p.get("corr-method", base.method)
+    budget = overrides.get("memory_budget") or p.get("corr-memory-budget", base.memory_budget)
+    if precision not in PRECISIONS:
+        raise ValueError(f"unknown corr-precision '{precision}', expected one of {list(PRECISIONS)}")
+    if method not in METHODS:
+        raise ValueError(f"unknown corr-method '{method}', expected one of {list(METHODS)}")
+    return CorrOptions(precision, method, _bytes(budget))
+
+
+_current = CorrOptions(DEFAULTS["corr-precision"], DEFAULTS["corr-method"], DEFAULTS["corr-memory-budget"])
+
+
+def configure(parameters=None, **overrides):
+    """Set the process-wide options from a cfg/model ``parameters`` mapping (what ``Model.from_config``
+    would call); returns the previous options (pass them back to ``restore``)."""
+    global _current
+    prev = _current
+    _current = corr_options(parameters, **overrides)
+    return prev
+
+
+def restore(opts):
+    global _current
+    _current = opts
+
+
+def current():
+    return _current
+
+
+def volume_bytes(batch, height, width, levels, precision, training):
+    """HBM bytes of the all-pairs path for a (batch, height, width) query grid: the pooled pyramid in
+    the precision's storage type, plus the dense fp32 pyramid gradient when training."""
+    n = height * width
+    t = sum((height >> l) * (width >> l) for l in range(levels))
+    b = batch * n * t * _STORAGE_BYTES[precision]
+    if training:
+        b += batch * n * (t + 8 * levels * height) * 4          # G over the 8-padded target rows
+    return b
+
+
+def choose_method(method, batch, height, width, levels, precision, training, budget):
+    """'volume' or 'otf' for a block: explicit methods pass through; 'auto' takes the volume while it
+    fits the budget."""
+    if method != "auto":
+        return method
+    return "otf" if volume_bytes(batch, height, width, levels, precision, training) > budget else "volume"

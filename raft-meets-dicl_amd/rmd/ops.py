@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from . import _lib, library
+from . import _lib, config, library
 from ._lib import RMD_BF16, RMD_BF16X3, RMD_F16, RMD_F32
 
 # precision modes: (GEMM compute type, pyramid storage type)
@@ -19,18 +19,17 @@ PRECISIONS = {
     "bf16-f32": (RMD_BF16, RMD_F32),  # bf16 operands, f32 pyramid
     "fp32-f16": (RMD_F32, RMD_F16),   # exact f32 GEMM, fp16 pyramid
 }
-_default_precision = "fp32"
 
 
 def set_default_precision(name):
-    global _default_precision
+    """Process-wide precision of blocks built with precision=None (rmd.config 'corr-precision')."""
     if name not in PRECISIONS:
         raise ValueError(f"unknown precision '{name}', expected one of {sorted(PRECISIONS)}")
-    _default_precision = name
+    config.configure(precision=name)
 
 
 def get_default_precision():
-    return _default_precision
+    return config.current().precision
 
 
 def _require_gpu(*tensors):
@@ -87,7 +86,7 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     _require_gpu(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
-    compute, storage = PRECISIONS[precision or _default_precision]
+    compute, storage = PRECISIONS[precision or get_default_precision()]
     b, c, h, w = fmap1.shape
     scale = 1.0 / float(c) ** 0.5 if scale is None else float(scale)
     d = library.describe(b, h, w, levels, storage)
@@ -134,7 +133,7 @@ def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
     _require_gpu(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
-    compute = PRECISIONS[precision or _default_precision][0]     # fp32: split bf16, fp32-exact: f32
+    compute = PRECISIONS[precision or get_default_precision()][0]     # fp32: split bf16, fp32-exact: f32
     b, c, h, w = fmap1.shape
     ws = torch.ops.rmd.corr_otf_prepare(fmap1, fmap2, levels, compute, float(scale))
     return OtfState(ws, b, c, h, w, levels, compute)
@@ -146,6 +145,99 @@ def otf_lookup(st, coords, radius, mask_costs=()):
         raise ValueError(f"coords must be (B,2,H,W)=({st.b},2,{st.h},{st.w}), got {tuple(coords.shape)}")
     return torch.ops.rmd.corr_otf_lookup(st.ws, coords, st.c, st.levels, st.compute, radius,
                                          _mask_bits(mask_costs, st.levels))
+
+
+# ---- on-the-fly lookup autograd (training without the volume) ----------------------------------
+#
+# Same token scheme as the volume path below: every lookup's backward turns its grad_out into a record
+# of patch weights (rmd_corr_otf_record, O(L*N*(2r+2)^2) floats, no volume), and the prepare's
+# backward — which autograd runs after all of them — computes d fmap1 / d fmap2 from all records in one
+# pass (rmd_corr_otf_backward: the union target box of a query tile swept once for every iteration).
+
+class _OtfState:
+    def __init__(self, otf, f1, f2, scale):
+        self.otf = otf
+        self.f1 = f1
+        self.f2 = f2
+        self.scale = scale
+        self.records = []
+        self.radius = None
+
+
+class _OtfPrepareFn(torch.autograd.Function):
+    """Autograd node of raft_fs.CorrBlock.__init__ (raft_fs.py:16-31) on the on-the-fly path."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, state):
+        ctx.state = state
+        return fmap1.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _gtoken):
+        st = ctx.state
+        o = st.otf
+        if not st.records:
+            return torch.zeros_like(st.f1), torch.zeros_like(st.f2), None
+        lib = _lib.lib()
+        nbytes = lib.rmd_corr_otf_backward_workspace_bytes(o.b, o.c, o.h, o.w, o.levels, o.compute)
+        if nbytes == 0:
+            raise ValueError(f"otf backward: unsupported sizes (C={o.c} must be <= 256)")
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=st.f1.device)
+        g1 = torch.empty_like(st.f1)
+        g2 = torch.empty_like(st.f2)
+        recs = (ctypes.c_void_p * len(st.records))(*[r.data_ptr() for r in st.records])
+        with torch.cuda.device(st.f1.device):
+            _lib.check(lib.rmd_corr_otf_backward(_ptr(st.f1), _ptr(st.f2), _ptr(o.ws), o.b, o.c, o.h, o.w, o.levels,
+                                                 float(st.scale), o.compute, st.radius, len(st.records), recs,
+                                                 _ptr(g1), _ptr(g2), _ptr(ws), _stream(st.f1)),
+                       "rmd_corr_otf_backward")
+        st.records = []
+        return g1, g2, None
+
+
+class _OtfLookupFn(torch.autograd.Function):
+    """Autograd node of raft_fs.CorrBlock.__call__ (raft_fs.py:33-87) on the on-the-fly path; coords carry
+    no gradient (raft.py:402)."""
+
+    @staticmethod
+    def forward(ctx, token, coords, state, radius, mask_costs):
+        out = otf_lookup(state.otf, coords, radius, mask_costs)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.mask = _mask_bits(mask_costs, state.otf.levels)
+        ctx.save_for_backward(coords.detach().float().contiguous())
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (co,) = ctx.saved_tensors
+        st = ctx.state
+        o = st.otf
+        if st.radius is not None and st.radius != ctx.radius:
+            raise ValueError("otf backward: all lookups of one block must use the same radius")
+        st.radius = ctx.radius
+        lib = _lib.lib()
+        rec = torch.empty(lib.rmd_corr_otf_record_bytes(o.b, o.h, o.w, o.levels, ctx.radius), dtype=torch.uint8,
+                          device=co.device)
+        g = gout.float().contiguous()
+        with torch.cuda.device(co.device):
+            _lib.check(lib.rmd_corr_otf_record(_ptr(g), _ptr(co), o.b, o.h, o.w, o.levels, ctx.radius, ctx.mask,
+                                               _ptr(rec), _stream(co)), "rmd_corr_otf_record")
+        st.records.append(rec)
+        return gout.new_zeros(()), None, None, None, None
+
+
+def otf_block_autograd(fmap1, fmap2, levels, precision, scale=1.0):
+    """On-the-fly operands + autograd token for a block whose feature maps require gradients."""
+    _require_gpu(fmap1, fmap2)
+    otf = otf_prepare(fmap1, fmap2, levels, precision, scale=scale)
+    st = _OtfState(otf, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous(), scale)
+    token = _OtfPrepareFn.apply(fmap1, fmap2, st)
+    return otf, st, token
+
+
+def otf_lookup_autograd(token, state, coords, radius, mask_costs=()):
+    return _OtfLookupFn.apply(token, coords, state, radius, tuple(mask_costs))
 
 
 # ---- RAFT correlation autograd (training) -------------------------------------------------------
@@ -254,7 +346,7 @@ def ctx_desc(st):
 def corr_block_autograd(fmap1, fmap2, levels, precision, scale=None):
     """Pyramid + autograd token for a CorrBlock whose feature maps require gradients."""
     _require_gpu(fmap1, fmap2)
-    precision = precision or _default_precision
+    precision = precision or get_default_precision()
     pyr = corr_pyramid(fmap1, fmap2, levels, precision, scale=scale)
     st = _CorrState(pyr, fmap1.detach().float().contiguous(), fmap2.detach().float().contiguous(), precision)
     token = _CorrPyramidFn.apply(fmap1, fmap2, st)

@@ -13,20 +13,40 @@ reference's autograd through grid_sample / avg_pool2d / matmul.  Coordinates get
 
 import torch
 
-from . import ops
+from . import config, ops
 
 
 class CorrBlock:
-    """Correlation volume for matching costs (drop-in for raft.CorrBlock)."""
+    """Correlation volume for matching costs (drop-in for raft.CorrBlock).
+
+    ``precision`` / ``method`` / ``memory_budget`` are the drop-in's op selection (rmd.config; None =
+    the process values, set from a cfg/model ``parameters`` section by rmd.config.configure): method
+    'volume' builds the all-pairs pyramid, 'otf' samples pooled features on the fly each lookup (no
+    O(N^2) memory; raft_fs semantics with this block's scale), 'auto' takes the volume while it fits
+    the memory budget.  Both are differentiable.
+    """
 
     scale = None            # 1/sqrt(C) (raft.py:33); raft_fs.CorrBlock overrides with 1.0
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, precision=None):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, precision=None, method=None, memory_budget=None):
+        opts = config.corr_options(None, precision=precision, method=method, memory_budget=memory_budget)
         self.num_levels = num_levels
         self.radius = radius
-        self.precision = precision or ops.get_default_precision()
+        self.precision = opts.precision
         self._state = self._token = None
-        if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
+        training = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        b, c, h, w = fmap1.shape
+        self.method = config.choose_method(opts.method, b, h, w, num_levels, self.precision, training,
+                                           opts.memory_budget)
+        scale = float(c) ** -0.5 if self.scale is None else float(self.scale)
+        if self.method == "otf":
+            self.pyramid = None
+            if training:
+                self._otf, self._state, self._token = ops.otf_block_autograd(fmap1, fmap2, num_levels, self.precision,
+                                                                             scale)
+            else:
+                self._otf = ops.otf_prepare(fmap1, fmap2, num_levels, self.precision, scale=scale)
+        elif training:
             self.pyramid, self._state, self._token = ops.corr_block_autograd(fmap1, fmap2, num_levels,
                                                                              self.precision, self.scale)
         else:
@@ -35,9 +55,15 @@ class CorrBlock:
     @property
     def corr_pyramid(self):
         """Levels in the reference layout (B, H, W, 1, H_i, W_i) — unpacked copies, for inspection."""
+        if self.pyramid is None:
+            raise AttributeError("corr_pyramid: this block runs on the fly (method='otf') and holds no volume")
         return [self.pyramid.unpack(i) for i in range(self.num_levels)]
 
     def __call__(self, coords, mask_costs=[]):
+        if self.method == "otf":
+            if self._token is not None and torch.is_grad_enabled():
+                return ops.otf_lookup_autograd(self._token, self._state, coords, self.radius, mask_costs)
+            return ops.otf_lookup(self._otf, coords, self.radius, mask_costs)
         if self._token is not None and torch.is_grad_enabled():
             return ops.corr_lookup_autograd(self._token, self._state, coords, self.radius, mask_costs)
         return ops.corr_lookup(self.pyramid, coords, self.radius, mask_costs)

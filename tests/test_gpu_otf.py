@@ -4,7 +4,9 @@ raft_fs.CorrBlock(method="otf") (reference src/models/impls/raft_fs.py:13-87) ag
 vectors the reference produced, against oracle.corr_lookup_fs (float64) on seeded inputs covering
 ragged sizes, channel counts that are not a multiple of the operand padding, masked levels, 1-pixel
 levels (NaN) and flow spreads that overflow the per-block target box (per-query fallback), and at the
-full cfg2 size against the volume path (same kernels' results must agree).
+full cfg2 size against the volume path (same kernels' results must agree).  The backward
+(rmd_corr_otf_record + rmd_corr_otf_backward) against the reference's autograd gradients
+(gen_golden_fs_backward.py), the float64 oracle over several lookups, and the volume path's backward.
 
 Tolerances (max|got-ref| / max|ref|): fp32 mode (split-bf16 MFMA, ~1e-5) and fp32-exact (f32 MFMA) 1e-4,
 bf16 mode 1e-2.
@@ -123,10 +125,120 @@ def test_otf_full_size_agrees_with_volume_path(precision):
     assert rel_max_err(a.cpu().numpy(), ref.cpu().numpy()) < TOL[precision]
 
 
-def test_otf_is_inference_only():
+def _grads(cb_factory, f1, f2, coords_list, gouts, mask=()):
+    t1 = _t(f1).requires_grad_(True)
+    t2 = _t(f2).requires_grad_(True)
+    cb = cb_factory(t1, t2)
+    loss = 0
+    for co, go in zip(coords_list, gouts):
+        loss = loss + (cb(_t(co), list(mask)) * _t(go)).sum()
+    g1, g2 = torch.autograd.grad(loss, (t1, t2))
+    torch.cuda.synchronize()
+    return cb, g1.cpu().numpy(), g2.cpu().numpy()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32-exact", "bf16"])
+@pytest.mark.parametrize("name", ["corr_fs_bwd_b2_c32_24x40", "corr_fs_bwd_b1_c48_21x35_l3r3"])
+def test_otf_backward_matches_reference_golden(precision, name):
+    """raft_fs.CorrBlock(method='otf') gradients against the reference's own autograd gradients
+    (tests/golden/gen_golden_fs_backward.py: avg_pool2d chain + grid_sample + matmul backward)."""
     import rmd
-    f1 = torch.randn(1, 8, 8, 8, device=DEV, requires_grad=True)
-    with pytest.raises(RuntimeError, match="inference-only"):
-        rmd.raft_fs.CorrBlock(f1, f1.detach(), 2, 2, method="otf")
-    with torch.no_grad():
-        rmd.raft_fs.CorrBlock(f1, f1.detach(), 2, 2, method="otf")
+    g = load_golden(name)
+    levels, r = int(g["levels"]), int(g["radius"])
+    mask = tuple(g["mask_costs"].tolist())
+    cb, g1, g2 = _grads(lambda a, b: rmd.raft_fs.CorrBlock(a, b, levels, r, precision=precision, method="otf"),
+                        g["fmap1"], g["fmap2"], [g["coords"]], [g["grad_out"]], mask)
+    assert cb.method == "otf"
+    assert rel_max_err(g1, g["grad_fmap1"]) < TOL[precision]
+    assert rel_max_err(g2, g["grad_fmap2"]) < TOL[precision]
+
+
+BWD_CASES = [
+    # b, c, h, w, levels, radius, spread, mask, lookups
+    (2, 32, 24, 40, 4, 4, 2.0, (), 3),            # several lookups accumulate into one backward
+    (1, 40, 17, 23, 3, 3, 3.0, (4,), 2),          # C not a multiple of 32, ragged map, level 1 masked
+    (1, 256, 46, 62, 4, 4, 4.0, (), 2),           # cfg1 feature shape
+    (1, 16, 30, 50, 2, 7, 25.0, (), 2),           # huge spread: wide union boxes (several bands per row)
+    (2, 8, 9, 70, 1, 1, 0.5, (), 35),             # 35 lookups: records split over two launches (32 max)
+]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", BWD_CASES, ids=[f"b{c[0]}c{c[1]}_{c[2]}x{c[3]}_l{c[4]}r{c[5]}_n{c[8]}"
+                                                for c in BWD_CASES])
+def test_otf_backward_matches_oracle(case, precision):
+    """Gradients of several on-the-fly lookups of one block (each with its own coords and upstream
+    gradient) against the float64 oracle summed over the lookups."""
+    import rmd
+    b, c, h, w, levels, r, spread, mask, n = case
+    rng = np.random.default_rng(c * 100 + w)
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    cos = [_grid_coords(rng, b, h, w, spread) for _ in range(n)]
+    d = (2 * r + 1) ** 2
+    gos = [rng.standard_normal((b, levels * d, h, w)).astype(np.float32) for _ in range(n)]
+    _, g1, g2 = _grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, levels, r, precision=precision, method="otf"),
+                       f1, f2, cos, gos, mask)
+    r1 = np.zeros(f1.shape)
+    r2 = np.zeros(f2.shape)
+    for co, go in zip(cos, gos):
+        a1, a2 = oracle.corr_lookup_fs_backward(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64),
+                                                levels, r, go.astype(np.float64), mask)
+        r1 += a1
+        r2 += a2
+    assert rel_max_err(g1, r1) < TOL[precision]
+    assert rel_max_err(g2, r2) < TOL[precision]
+
+
+def test_otf_backward_equals_volume_backward_raft_scale():
+    """rmd.raft.CorrBlock (scale 1/sqrt(C)) trained through the on-the-fly path gives the volume path's
+    gradients (fp32 mode, 12 lookups with a flow that moves every iteration, B=2 at the cfg2 map size)."""
+    import rmd
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    b, c, h, w = 2, 256, 55, 128
+    f1 = torch.randn(b, c, h, w, generator=gen).numpy()
+    f2 = torch.randn(b, c, h, w, generator=gen).numpy()
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    base = np.stack([xs, ys])[None].astype(np.float32)
+    drift = torch.randn(b, 2, 1, 1, generator=gen).numpy() * 4
+    cos = [(base + (k + 1) / 12 * drift + 0.5 * torch.randn(b, 2, h, w, generator=gen).numpy()).astype(np.float32)
+           for k in range(12)]
+    gos = [torch.randn(b, 324, h, w, generator=gen).numpy() for _ in range(12)]
+    cb_o, o1, o2 = _grads(lambda a, bb: rmd.raft.CorrBlock(a, bb, 4, 4, precision="fp32", method="otf"), f1, f2, cos, gos)
+    cb_v, v1, v2 = _grads(lambda a, bb: rmd.raft.CorrBlock(a, bb, 4, 4, precision="fp32", method="volume"), f1, f2, cos,
+                          gos)
+    assert cb_o.method == "otf" and cb_v.method == "volume"
+    assert rel_max_err(o1, v1) < 1e-4
+    assert rel_max_err(o2, v2) < 1e-4
+
+
+def test_auto_method_follows_memory_budget():
+    """method='auto' (the default) takes the volume while it fits the budget (rmd.config), else otf; the
+    two paths give the same lookup."""
+    import rmd
+    rng = np.random.default_rng(3)
+    f1 = _t(rng.standard_normal((1, 32, 24, 40)).astype(np.float32))
+    f2 = _t(rng.standard_normal((1, 32, 24, 40)).astype(np.float32))
+    co = _t(_grid_coords(rng, 1, 24, 40, 2.0))
+    big = rmd.raft_fs.CorrBlock(f1, f2, 4, 4)
+    small = rmd.raft_fs.CorrBlock(f1, f2, 4, 4, memory_budget=1 << 16)
+    assert big.method == "volume" and small.method == "otf"
+    prev = rmd.config.configure({"corr-method": "auto", "corr-memory-budget": "64KiB"})
+    try:
+        assert rmd.raft_fs.CorrBlock(f1, f2, 4, 4).method == "otf"
+    finally:
+        rmd.config.restore(prev)
+    assert rel_max_err(small(co).cpu().numpy(), big(co).cpu().numpy()) < 1e-4
+
+
+def test_otf_workspace_mismatch_raises():
+    """The operator checks the workspace against its sizes / compute mode (a bf16 workspace read as
+    fp32 would index past it)."""
+    from rmd import ops
+    f = torch.randn(1, 32, 12, 16, device=DEV)
+    st = ops.otf_prepare(f, f, 2, "bf16")
+    co = torch.zeros(1, 2, 12, 16, device=DEV)
+    with pytest.raises(ValueError, match="workspace"):
+        torch.ops.rmd.corr_otf_lookup(st.ws, co, 32, 2, ops.PRECISIONS["fp32"][0], 3, 0)
+    with pytest.raises(ValueError, match="workspace"):
+        torch.ops.rmd.corr_otf_lookup(st.ws, co, 64, 2, st.compute, 3, 0)
