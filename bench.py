@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--hybrid-batch", type=int, default=8, help="frame pairs per GPU (weak; --global-batch splits)")
     ap.add_argument("--dicl", choices=["on", "off"], default="on",
                     help="extra leg: DICL cost volumes + MatchingNet coarse-to-fine at 384x512 (BASELINE configs[2])")
+    ap.add_argument("--highres", choices=["on", "off"], default="on",
+                    help="extra key 'highres_fs': raft/fs inference at a 4K 1/8 map (270x480, C=256, b2, 12 lookups), "
+                         "on-the-fly lookup vs the all-pairs volume (rank 0 of single-GPU runs)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (pair with --backend gloo)")
@@ -482,6 +485,22 @@ def dicl_leg(args, world, rank, device):
             "data": "synthetic feature maps (encoder / context nets outside the hot path)"}
 
 
+def highres_leg(args, precision):
+    """SURVEY.md §8(f) rank 1 / raft_fs.py:13-87 at high resolution: a 4K frame pair (2160x3840 -> 1/8 map
+    270x480, C=256, batch 2) through raft_fs.CorrBlock with 12 lookups, once with the on-the-fly lookup
+    (no O(N^2) memory) and once with the all-pairs volume (an 89 GB fp16 pyramid at this size): the
+    crossover the 'auto' method's memory budget stands for (tools/bench_otf.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_otf
+    res = bench_otf.highres(precision, reps=3)
+    import rmd
+    res["auto_method_at_default_budget"] = rmd.config.choose_method("auto", 2, 270, 480, 4, precision, False,
+                                                                    rmd.config.current().memory_budget)
+    res["workload"] = ("raft/fs CorrBlock inference, 4K 1/8 map 270x480, C=256, b2, 4 levels, r=4, 12 lookups: "
+                       "on-the-fly vs all-pairs volume")
+    return res
+
+
 def progress(rank, what):
     """One stderr line per leg and rank (the JSON line stays the only stdout output): shows where a
     long multi-rank run is."""
@@ -795,6 +814,13 @@ def main():
                 torch.cuda.empty_cache()
             if rank == 0:
                 res[key] = out
+    if rank == 0 and world == 1 and not args.dry_run and args.highres == "on":
+        progress(rank, "highres_fs leg")
+        try:
+            res["highres_fs"] = highres_leg(args, args.precision)
+        except Exception as e:                          # noqa: BLE001 — reported in the JSON line
+            res["highres_fs"] = {"error": f"{type(e).__name__}: {e}"[:500]}
+        torch.cuda.empty_cache()
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             progress(rank, "cpu_baseline leg")

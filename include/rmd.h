@@ -300,6 +300,15 @@ int rmd_dicl_stack_int_warped_backward(const float* grad_mvol, const float* fmap
 int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose, float* out,
             void* stream);
 
+/* Weight gradient of rmd_dap (autograd of the 1x1 conv weight, blocks/dicl.py:137,147):
+ *   grad_weight[o][i] = sum_b sum_p grad_out[b, o, p] x[b, i, p]      (D x D, overwritten)
+ * split-bf16 MFMA (lo.hi + hi.lo + hi.hi, fp32 accumulation), the batch x pixel sum split over
+ * workgroups into `workspace` (rmd_dap_weight_grad_workspace_bytes) and summed in a fixed order
+ * (deterministic). */
+size_t rmd_dap_weight_grad_workspace_bytes(int batch, int disp, int pixels);
+int rmd_dap_weight_grad(const float* grad_out, const float* x, int batch, int disp, int pixels, float* grad_weight,
+                        void* workspace, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Per-iteration flow heads on either side of the lookup.
  */

@@ -2109,6 +2109,142 @@ extern "C" int rmd_dicl_stack_int_backward(const float* grad_mvol, const float* 
     return check_launch("rmd_dicl_stack_int_backward");
 }
 
+namespace rmd {
+namespace {
+
+// ---- DAP weight gradient ------------------------------------------------------------------------
+// dW[o][i] = sum_b sum_p g[b][o][p] x[b][i][p]: the weight gradient of the 1x1 convolution
+// (blocks/dicl.py:137,147; autograd of F.conv2d w.r.t. its weight).  M = N = D (tiny), K = B * pixels
+// (large): K is split over workgroups (one image's pixel chunk each), every workgroup computes the
+// full D x D partial with v_mfma_f32_32x32x16_bf16 on split operands (g = hi + lo, x = hi + lo:
+// lo.hi + hi.lo + hi.hi, the forward DAP's split), a second kernel sums the partials in split order
+// (deterministic).  Wave w of a workgroup owns a 2 x 2 block of 32 x 32 output tiles; A / B fragments
+// are 8 consecutive pixels of one row (two float4 loads) split in registers.
+constexpr int kWgPx = 16;                        // pixels per MFMA k-step
+
+__device__ __forceinline__ void wg_frag(const float* __restrict__ row, bool rok, int p, int n, dbf16x8_t& hi, dbf16x8_t& lo) {
+    float v[8];
+    if (rok && p + 7 < n && ((reinterpret_cast<uintptr_t>(row + p) & 15) == 0)) {
+        *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(row + p);
+        *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(row + p + 4);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (rok && p + e < n) ? row[p + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        hi[e] = (__bf16)v[e];
+        lo[e] = (__bf16)(v[e] - (float)hi[e]);
+    }
+}
+
+// grid (B * nchunk, tile groups); 256 threads; part (splits, Dp, Dp)
+__global__ void __launch_bounds__(256)
+dap_wgrad_kernel(const float* __restrict__ g, const float* __restrict__ x, int D, int n, int nchunk, int pchunk,
+                 int Dp, float* __restrict__ part) {
+    const int s = blockIdx.x, b = s / nchunk, c = s % nchunk;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane & 31, h = lane >> 5;
+    const int Dt = Dp / 32, Db = (Dt + 1) / 2;                   // 32-row tiles, 2x2 tile blocks per side
+    const int tb = blockIdx.y * 4 + w;
+    if (tb >= Db * Db) return;                                   // no barriers in this kernel
+    const int ot0 = 2 * (tb / Db), it0 = 2 * (tb % Db);
+    const int p0 = c * pchunk, p1 = min(n, p0 + pchunk);
+    const float* gb = g + (size_t)b * D * n;
+    const float* xb = x + (size_t)b * D * n;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) acc[u][v] = f32x16_t{};
+    const int o[2] = {32 * ot0 + j, 32 * (ot0 + 1) + j}, i[2] = {32 * it0 + j, 32 * (it0 + 1) + j};
+    for (int p = p0; p < p1; p += kWgPx) {
+        dbf16x8_t ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            wg_frag(gb + (size_t)min(o[u], D - 1) * n, o[u] < D, p + 8 * h, p1, ah[u], al[u]);
+            wg_frag(xb + (size_t)min(i[u], D - 1) * n, i[u] < D, p + 8 * h, p1, bh[u], bl[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[v], acc[u][v], 0, 0, 0);
+                acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[v], acc[u][v], 0, 0, 0);
+                acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bh[v], acc[u][v], 0, 0, 0);
+            }
+    }
+    // lane (column j, half h): register 4r + k is row 8r + 4h + k of the tile
+    float* ps = part + (size_t)s * Dp * Dp;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            if (ot0 + u >= Dt || it0 + v >= Dt) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = 32 * (ot0 + u) + 8 * (r >> 2) + 4 * h + (r & 3);
+                ps[(size_t)row * Dp + 32 * (it0 + v) + j] = acc[u][v][r];
+            }
+        }
+}
+
+// dW[o][i] = sum over splits in order (deterministic)
+__global__ void __launch_bounds__(256)
+dap_wgrad_reduce(const float* __restrict__ part, int splits, int D, int Dp, float* __restrict__ dw) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= D * D) return;
+    const int o = idx / D, i = idx % D;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[((size_t)k * Dp + o) * Dp + i];
+    dw[idx] = s;
+}
+
+struct WgPlan {
+    int Dp, groups, nchunk, pchunk, splits;
+};
+
+WgPlan wgrad_plan(int batch, int D, int n) {
+    WgPlan w{};
+    w.Dp = (D + 31) / 32 * 32;
+    const int Db = (w.Dp / 32 + 1) / 2;
+    w.groups = (Db * Db + 3) / 4;
+    // about 256 workgroups in all (one per CU), at least 4 k-steps per split
+    const int want = std::max(1, 256 / (w.groups * batch));
+    const int steps = (n + kWgPx - 1) / kWgPx;
+    const int per = std::max(4, (steps + want - 1) / want);
+    w.pchunk = per * kWgPx;
+    w.nchunk = (n + w.pchunk - 1) / w.pchunk;
+    w.splits = batch * w.nchunk;
+    return w;
+}
+
+}  // namespace
+}  // namespace rmd
+
+extern "C" size_t rmd_dap_weight_grad_workspace_bytes(int batch, int disp, int pixels) {
+    if (batch <= 0 || disp <= 0 || pixels <= 0) return 0;
+    const rmd::WgPlan w = rmd::wgrad_plan(batch, disp, pixels);
+    return (size_t)w.splits * w.Dp * w.Dp * sizeof(float);
+}
+
+extern "C" int rmd_dap_weight_grad(const float* grad_out, const float* x, int batch, int disp, int pixels,
+                                   float* grad_weight, void* workspace, void* stream) {
+    RMD_REQUIRE(grad_out && x && grad_weight && workspace, RMD_ERR_ARG, "rmd_dap_weight_grad: null pointer");
+    RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap_weight_grad: bad sizes");
+    const rmd::WgPlan w = rmd::wgrad_plan(batch, disp, pixels);
+    RMD_REQUIRE((long long)w.splits * w.groups < (1ll << 31) && w.groups < 65536, RMD_ERR_SHAPE,
+                "rmd_dap_weight_grad: grid too large");
+    hipStream_t st = rmd::as_stream(stream);
+    float* part = static_cast<float*>(workspace);
+    rmd::dap_wgrad_kernel<<<dim3(w.splits, w.groups), 256, 0, st>>>(grad_out, x, disp, pixels, w.nchunk, w.pchunk,
+                                                                    w.Dp, part);
+    int rc = rmd::check_launch("rmd_dap_weight_grad");
+    if (rc) return rc;
+    rmd::dap_wgrad_reduce<<<(disp * disp + 255) / 256, 256, 0, st>>>(part, w.splits, disp, w.Dp, grad_weight);
+    return rmd::check_launch("rmd_dap_weight_grad reduce");
+}
+
 extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp, int pixels, int transpose,
                        float* out, void* stream) {
     RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");

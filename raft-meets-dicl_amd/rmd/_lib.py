@@ -74,6 +74,8 @@ _SIGS = {
     "rmd_dicl_stack_int_warped": (_I, [_P, _P, _P] + [_I] * 6 + [_P, _P, _P]),
     "rmd_dicl_stack_int_warped_backward": (_I, [_P, _P, _P] + [_I] * 6 + [_P, _P, _P, _P]),
     "rmd_dap": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
+    "rmd_dap_weight_grad_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I]),
+    "rmd_dap_weight_grad": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
     "rmd_input_images": (_I, [_P, _I, _I, _I, _I, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               _I, _I, _I, _I, _I, _P, _P]),
     "rmd_input_flow": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P, _P]),

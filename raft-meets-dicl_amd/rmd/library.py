@@ -50,6 +50,7 @@ _SCHEMAS = {
                                        "int rv) -> (Tensor, Tensor)"),
     "dap": "dap(Tensor x, Tensor weight) -> Tensor",
     "dap_transpose": "dap_transpose(Tensor grad, Tensor weight) -> Tensor",
+    "dap_weight_grad": "dap_weight_grad(Tensor grad, Tensor x, int disp) -> Tensor",
     "up8": "up8(Tensor mask, Tensor flow, float temperature) -> Tensor",
     "up8_backward": "up8_backward(Tensor grad, Tensor mask, Tensor flow, float temperature) -> (Tensor, Tensor)",
     "softargmax": "softargmax(Tensor cost, int levels, int radius, float temperature) -> Tensor",
@@ -443,6 +444,28 @@ def _(grad, weight):
     return grad.new_empty(grad.shape, dtype=torch.float32)
 
 
+@_cuda("dap_weight_grad")
+def _dap_weight_grad(grad, x, disp):
+    """dW = sum_b g_b x_b^T (rmd_dap_weight_grad: split-bf16 MFMA, deterministic split-K)."""
+    b = x.shape[0]
+    if grad.shape != x.shape or x.numel() % (b * disp):
+        raise ValueError(f"dap_weight_grad: grad {tuple(grad.shape)} / x {tuple(x.shape)} with {disp} displacements")
+    gc, xc = _f32(grad), _f32(x)
+    n = xc.numel() // (b * disp)
+    lib = _lib.lib()
+    ws = torch.empty(lib.rmd_dap_weight_grad_workspace_bytes(b, disp, n), dtype=torch.uint8, device=xc.device)
+    out = torch.empty((disp, disp), dtype=torch.float32, device=xc.device)
+    with _Dev(xc) as st:
+        _lib.check(lib.rmd_dap_weight_grad(_ptr(gc), _ptr(xc), b, disp, n, _ptr(out), _ptr(ws), st),
+                   "rmd_dap_weight_grad")
+    return out
+
+
+@_fake("dap_weight_grad")
+def _(grad, x, disp):
+    return x.new_empty((disp, disp), dtype=torch.float32)
+
+
 def _dap_setup(ctx, inputs, output):
     x, weight = inputs
     ctx.save_for_backward(x, weight)
@@ -454,9 +477,7 @@ def _dap_bwd(ctx, grad):
     gx = torch.ops.rmd.dap_transpose(grad, weight) if ctx.needs_input_grad[0] else None
     gw = None
     if ctx.needs_input_grad[1]:
-        # plain library GEMM (hipBLASLt): dW = sum_b g_b x_b^T
-        g = grad.float().reshape(b, dd, -1)
-        gw = torch.matmul(g, x.float().reshape(b, dd, -1).transpose(1, 2)).sum(0).reshape(weight.shape).to(weight.dtype)
+        gw = torch.ops.rmd.dap_weight_grad(grad, x, dd).reshape(weight.shape).to(weight.dtype)
     return gx, gw
 
 

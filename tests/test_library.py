@@ -10,6 +10,7 @@ import pytest
 import torch
 
 EXPECTED = ["corr_lookup", "corr_otf_lookup", "corr_otf_prepare", "corr_pyramid", "dap", "dap_transpose",
+            "dap_weight_grad",
             "dicl_stack", "dicl_stack_backward", "dicl_stack_int", "dicl_stack_int_backward", "dicl_stack_int_warped",
             "dicl_stack_int_warped_backward", "softargmax", "softargmax_backward", "up8", "up8_backward",
             "warp_backwards", "warp_backwards_backward"]
@@ -64,6 +65,7 @@ def test_opcheck_operator_families():
         (torch.ops.rmd.dicl_stack, (f1.requires_grad_(), f2.requires_grad_(), co, 2, 0, 10, 12, False)),
         (torch.ops.rmd.dicl_stack_int, (f1, f2, 2, 2)),
         (torch.ops.rmd.dap, (r(2, 25, 10, 12).requires_grad_(), r(25, 25, 1, 1).requires_grad_())),
+        (torch.ops.rmd.dap_weight_grad, (r(2, 25, 10, 12), r(2, 25, 10, 12), 25)),
         (torch.ops.rmd.up8, (r(2, 576, 10, 12).requires_grad_(), r(2, 2, 10, 12).requires_grad_(), 4.0)),
         (torch.ops.rmd.softargmax, (r(2, 81, 10, 12).requires_grad_(), 1, 4, 1.0)),
     ]
