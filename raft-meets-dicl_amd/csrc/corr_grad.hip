@@ -18,12 +18,12 @@
 //
 // Geometry: one workgroup (8 waves, 2 per SIMD) owns a 256 (M) x 128 (Nc) output tile; wave
 // (wm = w & 3, wn = w >> 2) owns 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16.  K runs in
-// 64-deep chunks: the next chunk's fp32 operands are loaded into registers while the MFMAs of the
-// current chunk run, then split into hi / lo and written to LDS (one 272-B row per operand row:
-// hi 128 B | lo 128 B | 16 B pad = 17 x 16 B, so the 8-lane groups of a ds_read_b128 hit 8
-// distinct 16-B bank slots).  K is split over `splits` workgroups when the tile grid alone does not
-// fill the 256 CUs; the partial tiles go to a workspace and a second kernel sums them in a fixed
-// order (deterministic, no atomics).
+// 32-deep chunks through two LDS buffers (software pipeline, one barrier per chunk): chunk c+1's fp32
+// operands, loaded into registers during chunk c-1, are split into hi / lo and stored to the idle
+// buffer while chunk c's MFMAs read the other (one 144-B row per operand row: hi 64 B | lo 64 B | 16 B
+// pad = 9 x 16 B, so the 8-lane groups of a ds_read_b128 hit 8 distinct 16-B bank slots).  K is split
+// over `splits` workgroups when the tile grid alone does not fill the 256 CUs; the partial tiles go to
+// a workspace and a second kernel sums them in a fixed order (deterministic, no atomics).
 
 #include "rmd_common.h"
 
@@ -34,9 +34,10 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-constexpr int kTM = 256, kTN = 128, kKC = 64;
-constexpr int kRowB = 272;                                  // hi 128 B | lo 128 B | pad 16 B
-constexpr int kLdsA = kTM * kRowB, kLdsB = kTN * kRowB;     // 69,632 + 34,816 B
+constexpr int kTM = 256, kTN = 128, kKC = 32;
+constexpr int kRowB = 144;                                  // hi 64 B | lo 64 B | pad 16 B (9 x 16 B: odd)
+constexpr int kLdsA = kTM * kRowB, kLdsB = kTN * kRowB;     // 36,864 + 18,432 B per buffer
+constexpr int kLdsBuf = kLdsA + kLdsB;                      // one buffer: 55,296 B (two: 110,592 B)
 
 struct GemmArgs {
     const float* A;
@@ -73,13 +74,18 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ at, int k, int
     return v;
 }
 
-// VA / VB: 16-B aligned rows (row stride % 4 == 0) -> float4 loads; LAYOUT 0 / 1 as above
+// VA / VB: 16-B aligned rows (row stride % 4 == 0, aligned base) -> float4 loads; LAYOUT 0-3 as above.
+//
+// Software pipeline over 32-deep K chunks with two LDS buffers and one barrier per chunk: at the top
+// of chunk c the registers holding chunk c+1's fp32 operands are split into hi / lo and stored to the
+// other buffer, chunk c+2's loads are issued into the same registers, then the 24 MFMAs of chunk c run
+// from the current buffer; the barrier at the bottom publishes chunk c+1 and frees buffer c for c+2.
+// A global load thus has a whole chunk of MFMAs (two, for its first use) to land, and the hi / lo split
+// of the next chunk runs beside the current chunk's MFMAs (waves 0-3 and 4-7 share each SIMD).
 template <bool VA, bool VB, int LAYOUT>
 __global__ void __launch_bounds__(512, 1)
 grad_gemm_x3(GemmArgs p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* sA = smem;
-    unsigned char* sB = smem + kLdsA;
     const int nwg = gridDim.x;
     int id = xcd_block(blockIdx.x, nwg);       // consecutive ids (same batch, same A rows) share an XCD
     const int tn = id % p.ntn;
@@ -96,24 +102,24 @@ grad_gemm_x3(GemmArgs p) {
     const float* __restrict__ A = p.A + (size_t)b * p.sa;
     const float* __restrict__ Bm = p.Bm + (size_t)b * p.sb;
 
-    float4 ra[8], rb[4];
+    // per thread: A 4 x float4 (rows m0 + 64 it + tid / 8, k 4 (tid % 8) .. +3); B 2 x float4
+    float4 ra[4], rb[2];
     auto gload = [&](int k0) {
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const int row = m0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
+        for (int it = 0; it < 4; ++it) {
+            const int row = m0 + it * 64 + (tid >> 3), k = k0 + (tid & 7) * 4;
             ra[it] = row < p.M ? load4<VA>(A + (size_t)row * p.lda + k, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if constexpr (LAYOUT == 0 || LAYOUT == 2) {
-            // thread (kq, nq): k rows 4kq..4kq+3 of columns 4nq..4nq+3 — lanes (kq & 3, nq) of a wave
-            // read 4 k rows x 256 contiguous bytes; waves 0-3 / 4-7 take column halves 0-63 / 64-127
-            // (layout 2: 4 consecutive n of one 8-block are contiguous too)
+            // thread (kq, nq): k rows 2kq, 2kq + 1 of columns 4nq .. 4nq + 3 (16 kq per 16 lanes of a
+            // wave group: lanes (kq & 15, n) read 2 k rows x 64 contiguous bytes; waves 0-3 / 4-7 take
+            // column halves 0-63 / 64-127; layout 2: 4 consecutive n of one 8-block are contiguous too)
             const int kq = (lane & 3) | ((w & 3) << 2), n = n0 + 64 * (w >> 2) + 4 * (lane >> 2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int k = k0 + 4 * kq + r;
+            for (int r = 0; r < 2; ++r) {
+                const int k = k0 + 2 * kq + r;
                 rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (k < ke) {
-                    // address of element (k, n); n .. n + 3 follow it contiguously in both layouts
                     const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb + n
                                                    : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
                     if (VB && n + 3 < p.Nc) {
@@ -128,8 +134,8 @@ grad_gemm_x3(GemmArgs p) {
             }
         } else {
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const int row = n0 + it * 32 + (tid >> 4), k = k0 + (tid & 15) * 4;
+            for (int it = 0; it < 2; ++it) {
+                const int row = n0 + it * 64 + (tid >> 3), k = k0 + (tid & 7) * 4;
                 // layout 3: k .. k + 3 lie in one 8-block (k % 4 == 0), contiguous like layout 1's row
                 const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb + k
                                                : Bm + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7);
@@ -137,39 +143,40 @@ grad_gemm_x3(GemmArgs p) {
             }
         }
     };
-    auto lstore = [&]() {
+    auto lstore = [&](unsigned char* buf) {
+        unsigned char* sA = buf;
+        unsigned char* sB = buf + kLdsA;
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
+        for (int it = 0; it < 4; ++it) {
             bf16x4 hi, lo;
             split4(ra[it].x, ra[it].y, ra[it].z, ra[it].w, hi, lo);
-            unsigned char* d = sA + (it * 32 + (tid >> 4)) * kRowB + (tid & 15) * 8;
+            unsigned char* d = sA + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
             *reinterpret_cast<bf16x4*>(d) = hi;
-            *reinterpret_cast<bf16x4*>(d + 128) = lo;
+            *reinterpret_cast<bf16x4*>(d + 64) = lo;
         }
         if constexpr (LAYOUT == 0 || LAYOUT == 2) {
-            // transpose: column 4nq + j of the thread's 4 k rows -> LDS row of that column, k offset 4kq
+            // transpose: column 4nq + j of the thread's 2 k rows -> LDS row of that column, k offset 2kq
             const int kq = (lane & 3) | ((w & 3) << 2), nr = 64 * (w >> 2) + 4 * (lane >> 2);
-            const float c0[4] = {rb[0].x, rb[1].x, rb[2].x, rb[3].x};
-            const float c1[4] = {rb[0].y, rb[1].y, rb[2].y, rb[3].y};
-            const float c2[4] = {rb[0].z, rb[1].z, rb[2].z, rb[3].z};
-            const float c3[4] = {rb[0].w, rb[1].w, rb[2].w, rb[3].w};
+            const float c0[2] = {rb[0].x, rb[1].x}, c1[2] = {rb[0].y, rb[1].y};
+            const float c2[2] = {rb[0].z, rb[1].z}, c3[2] = {rb[0].w, rb[1].w};
             const float* cols[4] = {c0, c1, c2, c3};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                bf16x4 hi, lo;
-                split4(cols[j][0], cols[j][1], cols[j][2], cols[j][3], hi, lo);
-                unsigned char* d = sB + (nr + j) * kRowB + kq * 8;
-                *reinterpret_cast<bf16x4*>(d) = hi;
-                *reinterpret_cast<bf16x4*>(d + 128) = lo;
+                __bf16 h0 = (__bf16)cols[j][0], h1 = (__bf16)cols[j][1];
+                __bf16 l0 = (__bf16)(cols[j][0] - (float)h0), l1 = (__bf16)(cols[j][1] - (float)h1);
+                typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+                unsigned char* d = sB + (nr + j) * kRowB + kq * 4;
+                *reinterpret_cast<bf16x2*>(d) = bf16x2{h0, h1};
+                *reinterpret_cast<bf16x2*>(d + 64) = bf16x2{l0, l1};
             }
         } else {
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
+            for (int it = 0; it < 2; ++it) {
                 bf16x4 hi, lo;
                 split4(rb[it].x, rb[it].y, rb[it].z, rb[it].w, hi, lo);
-                unsigned char* d = sB + (it * 32 + (tid >> 4)) * kRowB + (tid & 15) * 8;
+                unsigned char* d = sB + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
                 *reinterpret_cast<bf16x4*>(d) = hi;
-                *reinterpret_cast<bf16x4*>(d + 128) = lo;
+                *reinterpret_cast<bf16x4*>(d + 64) = lo;
             }
         }
     };
@@ -182,36 +189,43 @@ grad_gemm_x3(GemmArgs p) {
 
     const int j32 = lane & 31, h = lane >> 5;
     const unsigned aoff = (unsigned)((wm * 64 + j32) * kRowB + h * 16);
-    const unsigned boff = (unsigned)((wn * 64 + j32) * kRowB + h * 16);
+    const unsigned boff = (unsigned)(kLdsA + (wn * 64 + j32) * kRowB + h * 16);
+    const int nchunk = (ke - kb + kKC - 1) / kKC;
 
+    // prologue: chunk 0 -> buffer 0, chunk 1 in flight in registers
     gload(kb);
-    for (int k0 = kb; k0 < ke; k0 += kKC) {
-        __syncthreads();                       // the previous chunk's fragment reads are done
-        lstore();
-        __syncthreads();
-        if (k0 + kKC < ke) gload(k0 + kKC);    // in flight during this chunk's MFMAs
+    lstore(smem);
+    if (nchunk > 1) gload(kb + kKC);
+    __syncthreads();
+    for (int c = 0; c < nchunk; ++c) {
+        unsigned char* cur = smem + (c & 1) * kLdsBuf;
+        if (c + 1 < nchunk) {
+            lstore(smem + ((c + 1) & 1) * kLdsBuf);             // chunk c+1: registers -> other buffer
+            if (c + 2 < nchunk) gload(kb + (c + 2) * kKC);      // chunk c+2 in flight during this chunk
+        }
 #pragma unroll
         for (int s = 0; s < kKC / 16; ++s) {
             bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const unsigned char* pa = sA + aoff + i * 32 * kRowB + s * 32;
-                const unsigned char* pb = sB + boff + i * 32 * kRowB + s * 32;
+                const unsigned char* pa = cur + aoff + i * 32 * kRowB + s * 32;
+                const unsigned char* pb = cur + boff + i * 32 * kRowB + s * 32;
                 ah[i] = *reinterpret_cast<const bf16x8*>(pa);
-                al[i] = *reinterpret_cast<const bf16x8*>(pa + 128);
+                al[i] = *reinterpret_cast<const bf16x8*>(pa + 64);
                 bh[i] = *reinterpret_cast<const bf16x8*>(pb);
-                bl[i] = *reinterpret_cast<const bf16x8*>(pb + 128);
+                bl[i] = *reinterpret_cast<const bf16x8*>(pb + 64);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    f32x16 c = acc[i][j];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c, 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c, 0, 0, 0);
+                    f32x16 t = acc[i][j];
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t, 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t, 0, 0, 0);
                 }
         }
+        __syncthreads();                                       // chunk c+1 published; buffer c free
     }
 
     // C tile (32 x 32): lane (j32, h) holds rows 8 (v >> 2) + 4 h + (v & 3) of column j32
@@ -290,8 +304,8 @@ void launch_gemm(const GemmArgs& a, int nwg, hipStream_t st) {
     // the >64 KB LDS opt-in is per device: set it before every launch (cheap host call), so a process
     // that launches on a second GPU gets it too
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kLdsA + kLdsB);
-    k<<<nwg, 512, kLdsA + kLdsB, st>>>(a);
+                              2 * kLdsBuf);
+    k<<<nwg, 512, 2 * kLdsBuf, st>>>(a);
 }
 
 }  // namespace
