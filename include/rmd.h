@@ -43,20 +43,34 @@ extern "C" {
 
 /*
  * Layout of a correlation pyramid in HBM (one allocation, `total_elements` elements of
- * `storage` type).  Level l has floor-halved sizes level_h[l] x level_w[l] (raft.py:38-47).  Each
- * target row is cut into chunks of tile_w[l] = 8, 8, 4, 2 elements (tile_h[l] = 1) and chunks are
- * QUERY-MINOR:
+ * `storage` type).  Level l has floor-halved sizes level_h[l] x level_w[l] (raft.py:38-47).  The
+ * target map of each level is cut into chunks of tile_h[l] x tile_w[l] elements and chunks are
+ * QUERY-MINOR: every chunk position holds the chunk of all `query_slots` queries back to back,
  *
  *   element(b, p, y, x) at level l =
- *     level_offset[l] + ((((b*tiles_y[l] + y/tile_h[l])*tiles_x[l] + x/tile_w[l]) * (H*W) + p)
- *                        * tile_h[l]*tile_w[l]) + (y%tile_h[l])*tile_w[l] + x%tile_w[l]
+ *     level_offset[l] + ((((b*tiles_y[l] + y/tile_h[l])*tiles_x[l] + x/tile_w[l]) * query_slots
+ *                         + slot(p)) * tile_h[l]*tile_w[l]) + (y%tile_h[l])*tile_w[l] + x%tile_w[l]
  *
- * with tiles_y[l] = level_h[l], tiles_x[l] = ceil(level_w[l] / tile_w[l]) and p = y1*W + x1 the
- * query pixel.  Consecutive queries' chunks of the same target row are adjacent, so a wave of 64
- * consecutive queries reads (lookup) and writes (GEMM epilogue) one row chunk as 64 x 16 B of
- * contiguous memory.  Padding columns of a level's last chunk hold unspecified
- * values and are never read.
+ * with tiles_y[l] = ceil(level_h[l] / tile_h[l]), tiles_x[l] = ceil(level_w[l] / tile_w[l]) and
+ * p = y1*W + x1 the query pixel.  Two layouts (`layout`):
+ *
+ *  RMD_LAYOUT_ROWS  (every GEMM except w8): chunks 1 x (8, 8, 4, 2), slot(p) = p, query_slots = H*W.
+ *  RMD_LAYOUT_TILES (the w8 GEMM: bf16 compute, fp16 storage): chunks 2x4, 2x4, 1x4, 1x2 and query
+ *    slots in 2 x 16 query tiles whose 8-slot groups are 2 x 4 query patches:
+ *      y1 < 2*floor(H/2): slot = ((y1/2)*QX + x1/16)*32 + ((x1%16)/4)*8 + (y1%2)*4 + x1%4, QX = ceil(W/16)
+ *      y1 = H-1, H odd  : slot = floor(H/2)*QX*32 + x1            (the last row in raster order)
+ *    query_slots = floor(H/2)*QX*32 (+ ceil(W/32)*32 for odd H); slots of no pixel (x1 >= W) hold
+ *    unspecified values.  A 128-B line of a level-0/1 chunk position then holds a 2 x 4 target patch
+ *    of a 2 x 4 query patch, so the windows of neighbouring queries share lines in both directions
+ *    (cfg2 lookup reads 55 MB modelled vs 66 MB in the row layout, tools/lookup_line_model.py).
+ *
+ * In both layouts consecutive slots' chunks are adjacent, so a wave of 64 consecutive slots reads
+ * (lookup) and writes (GEMM epilogue) 64 x 16 B of contiguous memory per chunk position (DESIGN.md
+ * §3).  Padding rows/columns of a level's last chunks hold unspecified values and are never read.
  */
+#define RMD_LAYOUT_ROWS 0
+#define RMD_LAYOUT_TILES 1
+
 typedef struct rmd_pyramid_desc {
     int batch, height, width;          /* query grid == level-0 target grid                  */
     int levels;                        /* 1 .. RMD_MAX_LEVELS                                */
@@ -66,11 +80,23 @@ typedef struct rmd_pyramid_desc {
     int tiles_y[RMD_MAX_LEVELS], tiles_x[RMD_MAX_LEVELS];
     long long level_offset[RMD_MAX_LEVELS];    /* in elements */
     long long total_elements;
+    int layout;                        /* RMD_LAYOUT_ROWS or RMD_LAYOUT_TILES                */
+    int query_slots;                   /* query positions per chunk position (>= H*W)        */
 } rmd_pyramid_desc;
 
-/* Fill `desc` for a (batch, height, width) query grid.  Host-only, no device work. */
+/* Fill `desc` for a (batch, height, width) query grid in the row layout.  Host-only, no device work. */
 int rmd_pyramid_describe(int batch, int height, int width, int levels, int storage,
                          rmd_pyramid_desc* desc);
+
+/* Same for an explicit layout (RMD_LAYOUT_TILES needs storage RMD_F16). */
+int rmd_pyramid_describe_layout(int batch, int height, int width, int levels, int storage, int layout,
+                                rmd_pyramid_desc* desc);
+
+/* Describe the pyramid rmd_corr_pyramid writes for (channels, compute): the tiles layout when the
+ * call runs the w8 GEMM (see rmd_corr_gemm_kernel), the row layout otherwise.  rmd_corr_pyramid
+ * rejects a desc whose layout its GEMM does not write. */
+int rmd_pyramid_describe_for(int batch, int height, int width, int levels, int storage, int channels,
+                             int compute, rmd_pyramid_desc* desc);
 
 /* Bytes of device workspace rmd_corr_pyramid needs for `compute` (operand staging). */
 size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* desc, int channels, int compute);

@@ -26,14 +26,18 @@ extern "C" const char* rmd_last_error(void) { return rmd::g_err; }
 
 extern "C" const char* rmd_version(void) { return "rmd 0.1 gfx950"; }
 
-extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels, int storage,
-                                    rmd_pyramid_desc* d) {
+extern "C" int rmd_pyramid_describe_layout(int batch, int height, int width, int levels, int storage, int layout,
+                                           rmd_pyramid_desc* d) {
     if (!d) {
         rmd::set_error("rmd_pyramid_describe: null desc");
         return RMD_ERR_ARG;
     }
     if (storage != RMD_F32 && storage != RMD_F16) {
         rmd::set_error("rmd_pyramid_describe: storage must be RMD_F32 or RMD_F16");
+        return RMD_ERR_ARG;
+    }
+    if (layout != RMD_LAYOUT_ROWS && !(layout == RMD_LAYOUT_TILES && storage == RMD_F16)) {
+        rmd::set_error("rmd_pyramid_describe: layout %d with storage %d (tiles need RMD_F16)", layout, storage);
         return RMD_ERR_ARG;
     }
     if (batch < 1 || height < 1 || width < 1 || levels < 1 || levels > RMD_MAX_LEVELS) {
@@ -47,7 +51,18 @@ extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels
     d->width = width;
     d->levels = levels;
     d->storage = storage;
-    const long long n = (long long)height * width;
+    d->layout = layout;
+    const bool tiles = layout == RMD_LAYOUT_TILES;
+    long long slots = (long long)height * width;
+    if (tiles) {
+        const long long qx = (width + 15) / 16;
+        slots = (long long)(height / 2) * qx * 32 + ((height & 1) ? (long long)(width + 31) / 32 * 32 : 0);
+    }
+    if (slots > 0x7fffffffLL) {
+        rmd::set_error("rmd_pyramid_describe: %lld query slots", slots);
+        return RMD_ERR_SHAPE;
+    }
+    d->query_slots = (int)slots;
     long long off = 0;
     int h = height, w = width;
     for (int l = 0; l < levels; ++l) {
@@ -56,19 +71,25 @@ extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels
             rmd::set_error("rmd_pyramid_describe: level %d of a %dx%d map is empty", l, height, width);
             return RMD_ERR_SHAPE;
         }
-        const int t = rmd::level_chunk(l);
+        const int th = tiles && l <= 1 ? 2 : 1;
+        const int tw = tiles ? (l <= 2 ? 4 : 2) : rmd::level_chunk(l);
         d->level_h[l] = h;
         d->level_w[l] = w;
-        d->tile_h[l] = 1;
-        d->tile_w[l] = t;
-        d->tiles_y[l] = h;
-        d->tiles_x[l] = (w + t - 1) / t;
+        d->tile_h[l] = th;
+        d->tile_w[l] = tw;
+        d->tiles_y[l] = (h + th - 1) / th;
+        d->tiles_x[l] = (w + tw - 1) / tw;
         d->level_offset[l] = off;
-        off += (long long)batch * d->tiles_y[l] * d->tiles_x[l] * n * t;
+        off += (long long)batch * d->tiles_y[l] * d->tiles_x[l] * slots * th * tw;
         h /= 2;
         w /= 2;
     }
     d->total_elements = off;
     rmd::clear_error();
     return RMD_OK;
+}
+
+extern "C" int rmd_pyramid_describe(int batch, int height, int width, int levels, int storage,
+                                    rmd_pyramid_desc* d) {
+    return rmd_pyramid_describe_layout(batch, height, width, levels, storage, RMD_LAYOUT_ROWS, d);
 }

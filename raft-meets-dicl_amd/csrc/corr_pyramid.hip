@@ -75,63 +75,58 @@ prep_operand(const float* __restrict__ f, T* __restrict__ o, int C, int N, int C
     for (int j = 0; j < (int)(16 * sizeof(T) / 16); ++j) dst[j] = src[j];
 }
 
-// prep (w8 GEMM path): fmap1 (B, C, N) f32 -> bf16 in MFMA B-fragment order,
-//   o[b][qt][s][lane][8]  (lane = j + 32h: channels 16s + 8h .. +7 of query min(32 qt + j, N - 1)),
-// so each of a wave's 16 B-fragment loads per 32-query tile is one contiguous 1 KiB read.  Padded
-// queries of the last tile copy query N-1 (their results are stored to N-1: identical bytes).
-__global__ void __launch_bounds__(kThreads)
-prep_bfrag(const float* __restrict__ f, __bf16* __restrict__ o, int C, int N, int nqt) {
-    const int b = blockIdx.y;
-    const int t = blockIdx.x * kThreads + threadIdx.x;
-    const int L = t & 63, s = (t >> 6) & 15, qt = t >> 10;
-    if (qt >= nqt) return;
-    const int j = L & 31, h = L >> 5;
-    const int q = min(qt * 32 + j, N - 1);
-    const int c0 = 16 * s + 8 * h;
-    const float* src = f + ((size_t)b * C + c0) * N + q;
-    bf16x8 v;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (__bf16)(c0 + e < C ? src[(size_t)e * N] : 0.f);
-    *reinterpret_cast<bf16x8*>(o + (((size_t)b * nqt + qt) * 1024 + s * 64 + L) * 8) = v;
-}
-
-// prep (w8 GEMM path, both operands in one launch): grid (128-pixel tiles, B, 2).  z = 0: fmap2 ->
-// A operand (B, N, 256) bf16 * scale; z = 1: fmap1 -> B operand in fragment order (prep_bfrag's
-// layout).  Read phase: a thread loads 8 channels x 4 pixels (float4 per channel row: a wave reads
-// 2 x 512 B contiguous per instruction), converts, and writes the 4 pixels' 16-B channel octets into
-// a pixel-major bf16 LDS tile.  Write phase: one 16-B fragment per lane-store, the tile's output is
-// one contiguous 64 KiB block for either operand.
+// prep (w8 GEMM path, both operands in one launch): grid (128-element tiles, B, 2).  z = 0: fmap2 ->
+// A operand (B, N, 256) bf16 * scale over raster pixels; z = 1: fmap1 -> B operand over the query
+// slots of the tiles layout (rmd.h), in MFMA B-fragment order
+//   o[b][qt][s][lane][8]  (lane = j + 32h: channels 16s + 8h .. +7 of slot 32 qt + j),
+// so each of a wave's 16 B-fragment loads per 32-query tile is one contiguous 1 KiB read.  Read
+// phase: a thread loads 8 channels x 4 pixels (a slot quad is 4 consecutive pixels of one row:
+// float4 per channel row), converts, and writes the 4 pixels' 16-B channel octets into a bf16 LDS
+// tile.  Write phase: one 16-B fragment per lane-store, the tile's output is one contiguous 64 KiB
+// block for either operand.  Slots of no pixel take a clamped pixel's features.
 constexpr int kPrepPx = 128, kPrepStride = 256 * 2 + 16;     // LDS row: 256 bf16 + 16 B pad
 
 __global__ void __launch_bounds__(512)
 prep_pair(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* __restrict__ opA,
-          __bf16* __restrict__ opB, int C, int N, int nqt, float scale) {
+          __bf16* __restrict__ opB, int C, int H, int W, int S, int nqt, float scale) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int b = blockIdx.y, which = blockIdx.z;
+    const int N = H * W;
     const float* f = which ? f1 : f2;
     const float s = which ? 1.0f : scale;
     const int t = threadIdx.x;
     const int p0 = blockIdx.x * kPrepPx;
-    const bool full = p0 + kPrepPx <= N && (N & 3) == 0;
-    const int pl = N - 1 - p0;                       // last valid pixel of the tile (clamp target)
+    if (p0 >= (which ? S : N)) return;               // block-uniform
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-        const int item = it * 512 + t;               // (channel octet cg, pixel quad q), q fastest
+        const int item = it * 512 + t;               // (channel octet cg, element quad q), q fastest
         const int q = item & 31, cg = item >> 5;
+        // the quad's first pixel (y1, x1) and whether all 4 are in the map and 16-B aligned
+        int y1, x1;
+        if (which) {
+            tiles_pixel(p0 + 4 * q, H, W, y1, x1);
+        } else {
+            y1 = 0;
+            x1 = p0 + 4 * q;                         // raster: row 0 of a 1 x N map
+        }
+        const int lim = which ? W : N;
+        const bool full = (which ? y1 < H : true) && x1 + 3 < lim && (lim & 3) == 0;
+        const int yc = which ? min(y1, H - 1) : 0;
+        const float* src = f + ((size_t)b * C) * N + (size_t)yc * (which ? W : 0);
         float v[8][4];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int c = cg * 8 + e;
-            const float* src = f + ((size_t)b * C + c) * N + p0 + 4 * q;
+            const float* row = src + (size_t)c * N;
             float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
             if (c < C) {
                 if (full) {
-                    x = *reinterpret_cast<const float4*>(src);
+                    x = *reinterpret_cast<const float4*>(row + x1);
                 } else {
-                    x.x = src[min(4 * q + 0, pl) - 4 * q];
-                    x.y = src[min(4 * q + 1, pl) - 4 * q];
-                    x.z = src[min(4 * q + 2, pl) - 4 * q];
-                    x.w = src[min(4 * q + 3, pl) - 4 * q];
+                    x.x = row[min(x1 + 0, lim - 1)];
+                    x.y = row[min(x1 + 1, lim - 1)];
+                    x.z = row[min(x1 + 2, lim - 1)];
+                    x.w = row[min(x1 + 3, lim - 1)];
                 }
             }
             v[e][0] = x.x * s;
@@ -645,35 +640,34 @@ corr_pyramid_stationary(const __bf16* __restrict__ opA, const __bf16* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------
-// Pipelined target-stationary kernel (bf16 operands, fp16 pyramid, C = 256): the performance path.
+// w8 GEMM (bf16 operands, fp16 pyramid in the tiles layout of rmd.h, C = 256): the performance path.
 //
-// Same block geometry as corr_pyramid_stationary<2> (4 waves, one per SIMD; a 16x16 target block's
-// A operand in LDS; each wave sweeps its own 32-query tiles against all 256 targets), but the
-// epilogue of tile t is interleaved k-step by k-step with the MFMAs of tile t+1:
-//  * two accumulator sets (2 x 128 AGPRs) ping-pong between "being accumulated" and "being stored";
-//  * k-step s of tile t+1 carries the epilogue piece s of tile t: level-0 row pair s/2, chunk s%2
-//    (one 1 KiB store), the level-1 partial sums of that pair, and every 4th / 8th k-step the
-//    level-1 / level-2 / level-3 stores, so ~27 VALU + 1-2 stores ride along each 8 MFMAs;
-//  * the B fragment of k-step s for tile t+2 is re-loaded into bq[s] right after k-step s's MFMAs
-//    (rolling refill), so each load has a whole tile-phase to land; the waits are hipcc's own;
-//  * stores are raw buffer stores through one descriptor per level covering the wave's valid rows:
-//    the per-lane 32-bit offset = query*chunk bytes + row*row stride, rows past the level and
-//    chunks past the row fall outside num_records / get a 1 GiB bias and are dropped by the
-//    hardware range check — no predication, no redirect;
-//  * lanes of a partial last query tile load (and so compute) query N-1's row and store to it:
-//    identical bytes to the same address, benign.
+// One workgroup (8 waves, two per SIMD) owns a 16x16 block of level-0 target pixels; its A operand
+// (256 targets x 256 channels bf16) stays in LDS while the waves sweep their own 32-query tiles
+// (query slots 32 qt .. 32 qt + 31 of the tiles layout: a 2 x 16 patch of query pixels).  Per tile
+// a wave runs 16 k-steps x 8 MFMA 32x32x16 tiles into 128 accumulator VGPRs, then the epilogue pools
+// in-lane and stores every level straight from registers:
+//  * in the 32x32 accumulator layout lane (j, h) holds, for query slot j, target rows 4i..4i+3 x
+//    columns 8cg + 4h .. +3 of MFMA tile (i, cg): a 2 x 4 level-0 chunk of the tiles layout is one
+//    lane's own 8 values (one 16-B store, lanes h = 0/1 writing neighbouring quads: each store
+//    instruction writes two contiguous 512-B runs); level-1 2 x 4 chunks and level-2 1 x 4 chunks
+//    need one v_permlane32_swap per row pair, level 3 one lane exchange;
+//  * stores are raw buffer stores through one descriptor per level covering the block's valid chunk
+//    rows: the per-lane 32-bit offset = slot * chunk bytes + quad * chunk stride (a 1 GiB bias for a
+//    quad past the level), rows past the level fall outside num_records and are dropped by the
+//    hardware range check — no predication, no redirect.  Slots of no pixel (x >= W) compute and
+//    store a clamped query's values into their own slot, so every 128-B line is written whole.
 namespace pipe {
 
 constexpr unsigned kBig = 0x40000000u;    // offset bias that lands beyond every level's range
 
 struct Lvl {
     __amdgpu_buffer_rsrc_t rsrc;
-    unsigned rs;      // row stride (bytes)
-    unsigned cs;      // chunk stride (bytes)
-    unsigned cw2;     // chunk bytes (per query)
-    int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
+    unsigned rs;      // chunk-row stride (bytes)
+    unsigned cs;      // chunk stride (bytes): next quad / chunk of the same chunk row
     unsigned hd;      // paired block (corr_pyramid_w8): added to the offsets of the block's second row
-                      // half, which holds the NEXT column block's rows: -(half rows) * rs + chunks * cs
+                      // half, which holds the NEXT column block's rows: chunks per block * cs - half rows * rs
+    int nq;           // valid chunks of this block's chunk rows (level 0: 0..4, 1: 0..2, 2-3: 0..1)
 };
 
 struct Ctx {
@@ -694,22 +688,24 @@ __device__ __forceinline__ void swp(unsigned& x, unsigned& y) {
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 typedef __attribute__((ext_vector_type(2))) int i32x2;
 
-// lane-dependent parts of the store offsets for query q (bytes): q * chunk bytes + h * row stride
+// lane-dependent parts of the store offsets of query slot q (bytes)
 struct LaneOff {
-    unsigned o[4];
+    unsigned o0[2];   // level 0, column group tc: quad 2 tc + h
+    unsigned o1;      // level 1: quad h
+    unsigned o2;      // level 2: chunk row h of each stored pair
+    unsigned o3;      // level 3: chunk row h
 };
 
-__device__ __forceinline__ LaneOff lane_offsets(const Ctx& c, int q, int h, bool live) {
+__device__ __forceinline__ LaneOff lane_offsets(const Ctx& c, int q, int h) {
     LaneOff r;
+    const unsigned uq = (unsigned)q;
 #pragma unroll
-    for (int l = 0; l < 4; ++l)
-        r.o[l] = live ? (unsigned)q * c.l[l].cw2 + (unsigned)h * (c.l[l].rs + (l == 3 ? c.l[3].hd : 0u)) : kBig;
+    for (int tc = 0; tc < 2; ++tc)
+        r.o0[tc] = 2 * tc + h < c.l[0].nq ? uq * 16u + (unsigned)(2 * tc + h) * c.l[0].cs : kBig;
+    r.o1 = h < c.l[1].nq ? uq * 16u + (unsigned)h * c.l[1].cs : kBig;
+    r.o2 = c.l[2].nq > 0 ? uq * 8u + (unsigned)h * c.l[2].rs : kBig;
+    r.o3 = c.l[3].nq > 0 ? uq * 4u + (unsigned)h * (c.l[3].rs + c.l[3].hd) : kBig;
     return r;
-}
-
-// uniform part of a store at (row pair base row r0, chunk tc) of level l
-__device__ __forceinline__ unsigned soff(const Lvl& L, int r0, int tc) {
-    return tc < L.chunks ? (unsigned)r0 * L.rs + (unsigned)tc * L.cs : kBig;
 }
 
 // per-tile running sums of the epilogue (unscaled: level-l sums are 4^l x the average)
@@ -720,49 +716,21 @@ struct EpiState {
 
 #define V(acc, row, cg, k) (acc[2 * ((row) >> 2) + (cg)][((row) & 3) * 4 + (k)])
 
-// Store context of block (rb, cb) for query tile qt in the query-tile-major layout (diagnostic
-// experiment): level l element (b, qt, y, xc, j, e) at off_l + ((((b NQT + qt) H_l + y) TX_l + xc) 32 + j) cw + e
-__device__ __forceinline__ Ctx ctx_qtm(const PyrGeom& g, int b, int qt, int rb, int cb, __half* pyr) {
-    Ctx c;
-    const int nqt = (g.height * g.width + 31) >> 5;
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
-        const int y0 = rb * span, xc0 = cb * nch;
-        const bool lv = l < g.levels;
-        const int cw = g.tw[l];
-        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
-        const unsigned rs = lv ? (unsigned)g.tx[l] * 32u * cw * 2u : 0u;
-        const size_t base = lv ? ((size_t)g.off[l] + ((((size_t)b * nqt + qt) * g.ty[l] + y0) * g.tx[l] + xc0) * 32 * cw) : 0;
-        __half* bp = pyr + base;
-        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
-        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
-        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
-                                                        (int)__builtin_amdgcn_readfirstlane((unsigned)rows * rs), 0x00020000);
-        c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
-        c.l[l].cs = __builtin_amdgcn_readfirstlane(32u * cw * 2u);
-        c.l[l].cw2 = (unsigned)cw * 2u;
-        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
-        c.l[l].hd = 0u;
-    }
-    return c;
-}
-
-// Epilogue piece s (0..15) of one tile, from accumulator set `acc` (see the block comment).
-template <int S, int AUX = 0>
+// Epilogue piece s (0..15) of one tile, from accumulator set `acc`: level-0 chunk row m = s/2 of
+// column group tc = s%2, the level-1 sums of those rows, and every 4th / 8th / 16th piece the level-1
+// / level-2 / level-3 stores — so the pieces can ride along the k-steps of the next tile.
+template <int S, int AUX>
 __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, const LaneOff& lo, EpiState& st) {
     constexpr int m = S >> 1, tc = S & 1;
-    // level 0: rows 2m (lanes h=0) / 2m+1 (lanes h=1) of chunk tc after the half-wave swap
+    // level 0: chunk rows 2m, 2m+1 x cols 8 tc + 4h .. +3 — this lane's own values
     {
-        unsigned x0 = pk(V(acc, 2 * m, tc, 0), V(acc, 2 * m, tc, 1));
-        unsigned x1 = pk(V(acc, 2 * m, tc, 2), V(acc, 2 * m, tc, 3));
-        unsigned y0 = pk(V(acc, 2 * m + 1, tc, 0), V(acc, 2 * m + 1, tc, 1));
-        unsigned y1 = pk(V(acc, 2 * m + 1, tc, 2), V(acc, 2 * m + 1, tc, 3));
-        swp(x0, y0);
-        swp(x1, y1);
-        const i32x4 d = {(int)x0, (int)x1, (int)y0, (int)y1};
+        const i32x4 d = {(int)pk(V(acc, 2 * m, tc, 0), V(acc, 2 * m, tc, 1)),
+                         (int)pk(V(acc, 2 * m, tc, 2), V(acc, 2 * m, tc, 3)),
+                         (int)pk(V(acc, 2 * m + 1, tc, 0), V(acc, 2 * m + 1, tc, 1)),
+                         (int)pk(V(acc, 2 * m + 1, tc, 2), V(acc, 2 * m + 1, tc, 3))};
         __builtin_amdgcn_raw_buffer_store_b128(d, c.l[0].rsrc,
-                                               (int)(lo.o[0] + soff(c.l[0], 2 * m, tc) + (m >= 4 ? c.l[0].hd : 0u)), 0, AUX);
+                                               (int)(lo.o0[tc] + (unsigned)m * c.l[0].rs + (m >= 4 ? c.l[0].hd : 0u)),
+                                               0, AUX);
     }
     // level-1 sums of level-1 row m, col group tc: cols {2h, 2h+1} (tc 0) / {4+2h, 5+2h} (tc 1)
 #pragma unroll
@@ -770,17 +738,19 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         st.s1[m][tc][u] = (V(acc, 2 * m, tc, 2 * u) + V(acc, 2 * m, tc, 2 * u + 1)) +
                           (V(acc, 2 * m + 1, tc, 2 * u) + V(acc, 2 * m + 1, tc, 2 * u + 1));
     if constexpr ((S & 3) == 3) {
-        // level-1 rows 2p, 2p+1 complete (p = S >> 2): one store of both rows, lanes h -> row 2p+h
+        // level-1 chunk row p (rows 2p, 2p+1) complete: lane h stores quad h (cols 4h .. 4h+3).  Per
+        // row, x = cols {2h, 2h+1}, y = cols {4+2h, 5+2h}; the swap leaves lanes h = 0 with cols 0-3
+        // and lanes h = 1 with cols 4-7 as (x, y)
         constexpr int p = S >> 2;
         unsigned x0 = pk(0.25f * st.s1[2 * p][0][0], 0.25f * st.s1[2 * p][0][1]);
-        unsigned x1 = pk(0.25f * st.s1[2 * p][1][0], 0.25f * st.s1[2 * p][1][1]);
-        unsigned y0 = pk(0.25f * st.s1[2 * p + 1][0][0], 0.25f * st.s1[2 * p + 1][0][1]);
+        unsigned y0 = pk(0.25f * st.s1[2 * p][1][0], 0.25f * st.s1[2 * p][1][1]);
+        unsigned x1 = pk(0.25f * st.s1[2 * p + 1][0][0], 0.25f * st.s1[2 * p + 1][0][1]);
         unsigned y1 = pk(0.25f * st.s1[2 * p + 1][1][0], 0.25f * st.s1[2 * p + 1][1][1]);
         swp(x0, y0);
         swp(x1, y1);
         const i32x4 d = {(int)x0, (int)y0, (int)x1, (int)y1};
         __builtin_amdgcn_raw_buffer_store_b128(d, c.l[1].rsrc,
-                                               (int)(lo.o[1] + soff(c.l[1], 2 * p, 0) + (p >= 2 ? c.l[1].hd : 0u)), 0, AUX);
+                                               (int)(lo.o1 + (unsigned)p * c.l[1].rs + (p >= 2 ? c.l[1].hd : 0u)), 0, AUX);
         // level-2 sums of level-2 row p: lane h holds cols {h, 2+h}
 #pragma unroll
         for (int cg = 0; cg < 2; ++cg)
@@ -794,7 +764,7 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         swp(x, y);          // lane h now holds row 2k+h: x = cols {0,2}, y = cols {1,3}
         const i32x2 d = {(int)__builtin_amdgcn_perm(y, x, 0x05040100u), (int)__builtin_amdgcn_perm(y, x, 0x07060302u)};
         __builtin_amdgcn_raw_buffer_store_b64(d, c.l[2].rsrc,
-                                              (int)(lo.o[2] + soff(c.l[2], 2 * k, 0) + (k >= 1 ? c.l[2].hd : 0u)), 0, AUX);
+                                              (int)(lo.o2 + (unsigned)(2 * k) * c.l[2].rs + (k >= 1 ? c.l[2].hd : 0u)), 0, AUX);
     }
     if constexpr (S == 15) {
         // level 3: rows 0, 1 (level-2 rows 0-1 / 2-3), cols 0, 1 (level-2 cols {0,1} / {2,3});
@@ -812,232 +782,16 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         const float inv = 1.0f / 64.0f;
         const unsigned v = pk(inv * (__uint_as_float(x0) + __uint_as_float(y0)),
                               inv * (__uint_as_float(x1) + __uint_as_float(y1)));
-        __builtin_amdgcn_raw_buffer_store_b32((int)v, c.l[3].rsrc, (int)(lo.o[3] + soff(c.l[3], 0, 0)), 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b32((int)v, c.l[3].rsrc, (int)lo.o3, 0, AUX);
     }
 }
 #undef V
 
-// A fragments of k-step s for the 8 target tiles (XOR-swizzled LDS rows, see the stationary kernel)
-__device__ __forceinline__ void lda(bf16x8 (&a)[8], const unsigned char* smem, const int (&arow)[8], int s, int h) {
-#pragma unroll
-    for (int ti = 0; ti < 8; ++ti) {
-        const int row = arow[ti];
-        a[ti] = *reinterpret_cast<const bf16x8*>(smem + (size_t)row * 512 + (((2 * s + h) ^ a_swz(row)) << 4));
-    }
-}
-
-// interleave hint for one k-step: 8 x {1 MFMA, 1 LDS read, 3 VALU}, then the memory ops
-__device__ __forceinline__ void kstep_schedule() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x040, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-}
-
-// One k-step S of a phase: MFMAs into accM (optional), epilogue piece S of accE (optional),
-// then refill bq[S] from bnext (the next tile).
-template <int S, bool MMA, bool EPI>
-__device__ __forceinline__ void kstep(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
-                                      bf16x8 (&acur)[8], bf16x8 (&anext)[8], const unsigned char* smem,
-                                      const int (&arow)[8], int h, const __bf16* bnext, const Ctx& c,
-                                      const LaneOff& lo, EpiState& st) {
-    if constexpr (MMA) {
-        if constexpr (S + 1 < 16) lda(anext, smem, arow, S + 1, h);
-        const f32x16 zero = {};
-#pragma unroll
-        for (int ti = 0; ti < 8; ++ti)
-            accM[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[ti], bq[S], S == 0 ? zero : accM[ti], 0, 0, 0);
-        bq[S] = *reinterpret_cast<const bf16x8*>(bnext + 16 * S);
-    }
-    if constexpr (EPI) epi_piece<S>(accE, c, lo, st);
-    if constexpr (MMA && EPI) kstep_schedule();
-    __builtin_amdgcn_sched_barrier(0);      // one scheduling region per k-step (bounded live ranges)
-}
-
-template <int S, bool MMA, bool EPI>
-__device__ __forceinline__ void ksteps(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
-                                       bf16x8 (&a0)[8], bf16x8 (&a1)[8], const unsigned char* smem,
-                                       const int (&arow)[8], int h, const __bf16* bnext, const Ctx& c,
-                                       const LaneOff& lo, EpiState& st) {
-    if constexpr (S < 16) {
-        if constexpr (S % 2 == 0) kstep<S, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
-        else kstep<S, MMA, EPI>(accM, accE, bq, a1, a0, smem, arow, h, bnext, c, lo, st);
-        ksteps<S + 1, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
-    }
-}
-
-// one tile-phase: MFMAs of the tile whose B fragments are in bq (if MMA), epilogue of the tile in
-// accE for query qE (if EPI), B fragments of the following tile loaded from bnext
-template <bool MMA, bool EPI>
-__device__ __forceinline__ void phase(f32x16 (&accM)[8], const f32x16 (&accE)[8], bf16x8 (&bq)[16],
-                                      const unsigned char* smem, const int (&arow)[8], int h, const __bf16* bnext,
-                                      const Ctx& c, int qE, bool live) {
-    bf16x8 a0[8], a1[8];
-    if constexpr (MMA) lda(a0, smem, arow, 0, h);
-    const LaneOff lo = lane_offsets(c, qE, h, live);
-    EpiState st;
-    ksteps<0, MMA, EPI>(accM, accE, bq, a0, a1, smem, arow, h, bnext, c, lo, st);
-}
-
 }  // namespace pipe
 
-#ifdef RMD_DIAG   // software-pipelined 4-wave variant: A/B only (tools/gemm_ab.py, librmd_diag.so)
-__global__ void __launch_bounds__(256, 1)
-corr_pyramid_pipe(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
-                  __half* __restrict__ pyr, int drop_stores) {
-    constexpr int Cp = 256, CPR = Cp / 8;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-    const int H = g.height, W = g.width, N = H * W;
-    const int ncb = (W + 15) >> 4;
-    const int nblk = ((H + 15) >> 4) * ncb;
-    // XCD-aware bijective remap: consecutive logical blocks (same batch) share an XCD's L2
-    const int nwg = gridDim.x;
-    const int orig = blockIdx.x;
-    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int lid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
-    const int tb = lid % nblk;
-    const int rest = lid / nblk;
-    const int split = rest % qsplit;
-    const int b = rest / qsplit;
-    const int rb = tb / ncb, cb = tb - rb * ncb;
-    const int ty0 = rb * 16, tx0 = cb * 16;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & 31, h = lane >> 5;
-
-    // ---- A block -> LDS (zero rows for targets outside the image) ------------------------------
-    const __bf16* gA = opA + (size_t)b * N * Cp;
-    for (int id = tid; id < 256 * CPR; id += 256) {
-        const int row = id / CPR, c = id - row * CPR;
-        const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
-        *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
-    }
-    __syncthreads();
-
-    int arow[8];
-#pragma unroll
-    for (int ti = 0; ti < 8; ++ti) arow[ti] = (4 * (ti >> 1) + (j >> 3)) * 16 + 8 * (ti & 1) + (j & 7);
-
-    // ---- per-level store descriptors of this block (wave-uniform) -------------------------------
-    pipe::Ctx c;
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
-        const int y0 = rb * span, xc0 = cb * nch;
-        const bool lv = l < g.levels;
-        const int cw = g.tw[l];
-        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
-        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 2u : 0u;
-        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;   // diagnostic: 0 drops every store
-        __half* bp = pyr + base;
-        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
-        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
-        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(range), 0x00020000);
-        c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
-        c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
-        c.l[l].cw2 = (unsigned)cw * 2u;
-        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
-        c.l[l].hd = 0u;
-    }
-
-    // ---- this wave's query tiles: t_k = first + k * stride, k < n -------------------------------
-    const __bf16* gB = opB + (size_t)b * N * Cp + 8 * h;
-    const int nqt = (N + 31) >> 5;
-    const int stride = 4 * qsplit;
-    const int first = split * 4 + w;
-    if (first >= nqt) return;
-    const int n = (nqt - first + stride - 1) / stride;
-    auto qrow = [&](int k) {        // B row of this lane for tile k (clamped: tile and query)
-        const int kk = min(k, n - 1);
-        return gB + (size_t)min((first + kk * stride) * 32 + j, N - 1) * Cp;
-    };
-    auto qidx = [&](int k) { return min((first + k * stride) * 32 + j, N - 1); };
-
-    bf16x8 bq[16];
-    {
-        const __bf16* p0 = qrow(0);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 16 * s);
-    }
-    f32x16 accA[8], accB[8];
-    // phases: MFMA of tile k alongside the epilogue of tile k-1.  Uniform two-phase loop body (the
-    // accumulator sets never move); a trailing tile index >= n computes on clamped rows and its
-    // epilogue stores are dropped (live = false -> offsets beyond every range).
-    pipe::phase<true, false>(accA, accB, bq, smem, arow, h, qrow(1), c, 0, false);      // MFMA tile 0
-    for (int k = 1; k <= n; k += 2) {
-        pipe::phase<true, true>(accB, accA, bq, smem, arow, h, qrow(k + 1), c, qidx(k - 1), true);
-        pipe::phase<true, true>(accA, accB, bq, smem, arow, h, qrow(k + 2), c, qidx(min(k, n - 1)), k < n);
-    }
-}
-#endif  // RMD_DIAG
-
-// ---------------------------------------------------------------------------------------------
-// 8-wave target-stationary kernel (bf16 operands, fp16 pyramid, C = 256).
-//
-// Same block geometry and epilogue as corr_pyramid_pipe, but two waves per SIMD instead of one
-// software-pipelined wave: each of the 8 waves owns whole 256-target x 32-query tiles (its own
-// query tiles, no duplicated B loads) and runs MFMAs then the epilogue serially; the SIMD's other
-// wave fills the matrix pipe while one stores.  Register budget 256 per wave: one accumulator set
-// (128), B fragments (64), A fragments single-buffered (32: the k-step s+1 fragment of tile ti is
-// read right after tile ti's k-step-s MFMA has consumed the register).
 namespace w8 {
 
-// A fragment of target tile ti at k-step s lives at LDS byte
-//   lane_base + ((2s ^ c) << 4) + tile_off(ti),   lane_base = (16 (j>>3) + (j&7)) * 512,
-// c = h ^ a_swz(row) (the swizzle of a fragment row does not depend on ti), tile_off(ti) =
-// (64 (ti>>1) + 8 (ti&1)) * 512 — so one address VGPR per k-step (two: tile_off of ti >= 4 passes
-// the 16-bit ds offset) and the tile offset in the instruction's immediate.
-template <int S>
-__device__ __forceinline__ unsigned step_addr(unsigned lane_base, unsigned c) {
-    return lane_base + (((unsigned)(2 * S) ^ c) << 4);
-}
-
-__device__ __forceinline__ bf16x8 lds_frag(const unsigned char* smem, unsigned v0, int ti) {
-    const unsigned off = (unsigned)(64 * (ti >> 1) + 8 * (ti & 1)) * 512u;
-    return *reinterpret_cast<const bf16x8*>(smem + v0 + off);
-}
-
-template <int S>
-__device__ __forceinline__ void mma_steps(f32x16 (&acc)[8], bf16x8 (&bq)[16], bf16x8 (&a)[8],
-                                          const unsigned char* smem, unsigned lane_base, unsigned c,
-                                          const __bf16* bnext) {
-    if constexpr (S < 16) {
-        const f32x16 zero = {};
-        const unsigned vn = step_addr<(S + 1) & 15>(lane_base, c);
-#pragma unroll
-        for (int ti = 0; ti < 8; ++ti) {
-            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ti], bq[S], S == 0 ? zero : acc[ti], 0, 0, 0);
-            if constexpr (S + 1 < 16) a[ti] = lds_frag(smem, vn, ti);     // single-buffered: reuse a[ti]
-        }
-        // rolling refill: k-step S's B fragment of the NEXT tile loads as soon as this k-step's
-        // MFMAs have consumed the register, a whole tile phase before it is needed
-        if (bnext) bq[S] = *reinterpret_cast<const bf16x8*>(bnext + 512 * S);
-        mma_steps<S + 1>(acc, bq, a, smem, lane_base, c, bnext);
-    }
-}
-
-__device__ __forceinline__ void mma(f32x16 (&acc)[8], bf16x8 (&bq)[16], const unsigned char* smem,
-                                    unsigned lane_base, unsigned c, const __bf16* bnext = nullptr) {
-    // keep the per-k-step addresses inside the tile loop (hoisted, 16-32 of them would spill)
-    asm volatile("" : "+v"(lane_base), "+v"(c));
-    bf16x8 a[8];
-    const unsigned v0 = step_addr<0>(lane_base, c);
-#pragma unroll
-    for (int ti = 0; ti < 8; ++ti) a[ti] = lds_frag(smem, v0, ti);
-    mma_steps<0>(acc, bq, a, smem, lane_base, c, bnext);
-}
-
-// ---- padded, swizzle-free A layout (PAD = true) -------------------------------------------------
+// ---- padded, swizzle-free A layout -------------------------------------------------------------
 // LDS row of block target (y, x) = (x>>3)*128 + y*8 + (x&7), rows 528 B apart (256 bf16 + 16 B pad).
 // The 32 targets of MFMA tile ti (4 rows x 8 cols) are then the consecutive LDS rows
 // (ti&1)*128 + (ti>>1)*32 + j, so lane (j, h)'s fragment of tile ti at k-step s sits at
@@ -1046,50 +800,10 @@ __device__ __forceinline__ void mma(f32x16 (&acc)[8], bf16x8 (&bq)[16], const un
 // Banks: 528 B = 33 x 16 B, so a ds_read_b128 lane group's 16 rows land in 16-B slots (row + chunk)
 // mod 16 = j mod 16 over lanes {0-3,12-15,20-27} and {4-11,16-19,28-31}: conflict-free, no XOR.
 constexpr unsigned kPadRow = 528;
-#ifndef RMD_W8_SCHED
-#define RMD_W8_SCHED 0
-#endif
 
 __device__ __forceinline__ int pad_row(int y, int x) { return ((x >> 3) << 7) + (y << 3) + (x & 7); }
 
-template <int S>
-__device__ __forceinline__ void mma_steps_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16], bf16x8 (&a)[8],
-                                              const unsigned char* smem, unsigned b0, unsigned b1) {
-    if constexpr (S < 16) {
-        const f32x16 zero = {};
-#pragma unroll
-        for (int ti = 0; ti < 8; ++ti) {
-            acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ti], bq[S], S == 0 ? zero : acc[ti], 0, 0, 0);
-            // single-buffered: k-step S+1's fragment of tile ti replaces the one this MFMA consumed, so
-            // it has the 7 other MFMAs of the k-step (~224 cycles) to land
-            if constexpr (S + 1 < 16)
-                a[ti] = *reinterpret_cast<const bf16x8*>(smem + ((ti & 1) ? b1 : b0) +
-                                                         (unsigned)((ti >> 1) * 32 * kPadRow + 32 * (S + 1)));
-        }
-#if RMD_W8_SCHED == 1
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);          // 1 MFMA
-            if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // then 1 DS read
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#elif RMD_W8_SCHED == 2
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        mma_steps_pad<S + 1>(acc, bq, a, smem, b0, b1);
-    }
-}
-
-__device__ __forceinline__ void mma_pad(f32x16 (&acc)[8], const bf16x8 (&bq)[16], const unsigned char* smem,
-                                        unsigned b0, unsigned b1) {
-    bf16x8 a[8];
-#pragma unroll
-    for (int ti = 0; ti < 8; ++ti)
-        a[ti] = *reinterpret_cast<const bf16x8*>(smem + ((ti & 1) ? b1 : b0) + (unsigned)((ti >> 1) * 32 * kPadRow));
-    mma_steps_pad<0>(acc, bq, a, smem, b0, b1);
-}
-
-// ---- B-ring variant (RING = true): B fragments stream through an 8-slot register ring ----------
+// ---- B-fragment register ring ------------------------------------------------------------------
 // k-step s of every tile lives in slot s % 8 and is loaded 7 k-steps (56 MFMAs) ahead — the previous
 // tile's k-steps 9-15 load this tile's 0-6 — instead of all 16 (64 VGPRs) being held for the whole
 // tile; the 32 VGPRs freed double-buffer the A fragments: k-step s+1's 8 fragments are read at the
@@ -1136,7 +850,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[8], const pipe::Ctx
     }
 }
 
-// Balanced schedule (host: w8_balance; product PP kernel only).
+// Balanced schedule (host: w8_balance).
 //  * pair: the last block row has at most 8 valid target rows and W % 32 == 0, so two horizontally
 //    adjacent last-row blocks share one workgroup: rows 0-7 of its virtual 16x16 block are block
 //    cb's rows, rows 8-15 block cb+1's (A staging and the stores' second-half delta Lvl::hd follow),
@@ -1153,23 +867,28 @@ struct Bal {
 
 }  // namespace w8
 
-// VPAD (ping-pong kernel): one branch per phase pair + vmcnt_pad_n after the ring prologue (product;
-// the diagnostic build's RMD_W8_VPAD=0 compiles the previous form for A/B)
-template <int AUX, bool ROLL, bool PAD = true, bool RING = false, bool PP = false, int ABL = 0, bool VPAD = true>
+// Ping-pong phases: the two waves of each SIMD (w and w + 4) alternate an MFMA phase and an epilogue
+// phase, separated by workgroup barriers, so one wave's pooling VALU and stores run while its partner
+// owns the matrix pipe (free-running partners drift into lock step: PMC of the free-running kernel
+// showed VALU co-issued with MFMA in a third of its VALU cycles; 0.221 vs 0.242 ms,
+// profiles/gemm_ab_r02_pp.json).  AUX = cache-policy bits of the pyramid stores (2 = non-temporal:
+// 0.213-0.216 vs 0.305-0.309 ms plain, profiles/gemm_ab_r02_cpol.json).
+template <int AUX>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, PyrGeom g, int qsplit,
-                __half* __restrict__ pyr, int drop_stores, int stagger, w8::Bal bal) {
+                __half* __restrict__ pyr, w8::Bal bal) {
     constexpr int Cp = 256, CPR = Cp / 8, WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
     const int H = g.height, W = g.width, N = H * W;
     const int ncb = (W + 15) >> 4;
     const int nrb = (H + 15) >> 4;
+    const int nqt = g.slots >> 5;                 // query tiles (tiles layout: slots % 32 == 0)
     // blocks per image: full blocks, then (pair) the last row's blocks two per workgroup
     const int nfull = bal.pair ? (nrb - 1) * ncb : nrb * ncb;
     const int nblk = nfull + (bal.pair ? ncb / 2 : 0);
     const int orig = blockIdx.x;
-    int lid, q_lo = 0, q_hi = (N + 31) >> 5;
+    int lid, q_lo = 0, q_hi = nqt;
     if (orig < bal.nprim) {
         // primaries: XCD-aware remap over the primary range (XCD k runs the k-th eighth)
         const int nwg = bal.nprim;
@@ -1205,222 +924,104 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
         const int ty = ty0 + (row >> 4) - (second ? 8 : 0), tx = tx0 + (row & 15) + (second ? 16 : 0);
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
-        if constexpr (PAD)
-            *reinterpret_cast<uint4*>(smem + (size_t)w8::pad_row(row >> 4, row & 15) * w8::kPadRow + c * 16) = v;
-        else
-            *reinterpret_cast<uint4*>(smem + (size_t)row * Cp * 2 + ((c ^ a_swz(row)) << 4)) = v;
+        *reinterpret_cast<uint4*>(smem + (size_t)w8::pad_row(row >> 4, row & 15) * w8::kPadRow + c * 16) = v;
     }
     __syncthreads();
 
-    const unsigned lane_row = 16u * (j >> 3) + (j & 7);
-    const unsigned lane_base = lane_row * 512u;
-    const unsigned lane_c = (unsigned)(h ^ a_swz((int)lane_row));
     const unsigned pb0 = (unsigned)j * w8::kPadRow + 16u * h, pb1 = pb0 + 128u * w8::kPadRow;
 
+    // store context per level: chunk rows cr0 .. of this block (th = 2, 2, 1, 1 target rows each),
+    // chunks cc0 .. (tw = 4, 4, 4, 2 columns)
     pipe::Ctx c;
+    const unsigned S = (unsigned)g.slots;
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
-        const int span = 16 >> l, nch = l == 0 ? 2 : 1;
-        const int y0 = rb * span, xc0 = cb * nch;
+        const int crows = l <= 1 ? 8 >> l : 4 >> (l - 2);       // chunk rows per 16-row block: 8, 4, 4, 2
+        const int cpb = l == 0 ? 4 : (l == 1 ? 2 : 1);          // chunks per 16-column block
+        const int cbytes = l <= 1 ? 16 : (l == 2 ? 8 : 4);      // chunk bytes
+        const int cr0 = rb * crows, cc0 = cb * cpb;
         const bool lv = l < g.levels;
-        const int cw = g.tw[l];
-        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
-        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 2u : 0u;
-        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-#ifdef RMD_DIAG
-        const unsigned range = drop_stores ? 0u : (unsigned)rows * rs;    // ablation: drop every store
-#else
-        const unsigned range = (unsigned)rows * rs;
-#endif
-        __half* bp = pyr + base;
+        const int rows = lv ? max(0, min(crows, g.ty[l] - cr0)) : 0;
+        const unsigned cs = S * (unsigned)cbytes;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * cs : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] * 2 + (((size_t)b * g.ty[l] + cr0) * g.tx[l] + cc0) * (size_t)cs) : 0;
+        const unsigned char* bp = reinterpret_cast<const unsigned char*>(pyr) + base;
         const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
         const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
-        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(range), 0x00020000);
+        c.l[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+                                                        (int)__builtin_amdgcn_readfirstlane((unsigned)rows * rs), 0x00020000);
         c.l[l].rs = __builtin_amdgcn_readfirstlane(rs);
-        c.l[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 2u);
-        c.l[l].cw2 = (unsigned)cw * 2u;
-        c.l[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
-        c.l[l].hd = paired ? __builtin_amdgcn_readfirstlane(nch * (unsigned)N * cw * 2u - (unsigned)(span / 2) * rs) : 0u;
+        c.l[l].cs = __builtin_amdgcn_readfirstlane(cs);
+        c.l[l].nq = __builtin_amdgcn_readfirstlane(lv ? max(0, min(cpb, g.tx[l] - cc0)) : 0);
+        c.l[l].hd = paired ? __builtin_amdgcn_readfirstlane((unsigned)cpb * cs - (unsigned)(crows / 2) * rs) : 0u;
     }
 
-    const int nqt = (N + 31) >> 5;
-    // B operand in fragment order (prep_bfrag): tile qt, k-step s = 1 KiB at ((b nqt + qt) 16 + s) KiB
+    // B operand in fragment order (prep_pair): tile qt, k-step s = 1 KiB at ((b nqt + qt) 16 + s) KiB
     const __bf16* gB = opB + ((size_t)b * nqt * 1024 + lane) * 8;
     const int stride = WAVES * qsplit;
-    int qt = split * WAVES + w;
-    if constexpr (RING && PP) {
-        // Ping-pong: the two waves of each SIMD (w and w + 4) alternate between an MFMA phase and an
-        // epilogue phase, separated by workgroup barriers, so one wave's pooling VALU and stores run
-        // while its partner owns the matrix pipe (free-running partners drift into lock step: PMC of
-        // the free-running kernel shows VALU co-issued with MFMA in only a third of its VALU cycles).
-        // Waves 4-7 start one phase late; every wave runs 2 * nmax + 1 barriers.
-        // this workgroup's query tiles: [q_lo, q_hi) (all of them unless helpers split the block)
-        const int f0 = q_lo + split * WAVES;
-        qt = f0 + w;
-        const int nmax = f0 < q_hi ? (q_hi - f0 + stride - 1) / stride : 0;
-        const int nw = qt < q_hi ? (q_hi - qt + stride - 1) / stride : 0;
-        const bool late = w >= 4;
-        unsigned b0 = pb0, b1 = pb1;
-        asm volatile("" : "+v"(b0), "+v"(b1));
-        bf16x8 ring[w8::kRing];
-        if (nw > 0) {
-#pragma unroll
-            for (int s = 0; s < w8::kRing - 1; ++s) ring[s] = *reinterpret_cast<const bf16x8*>(gB + (size_t)qt * 8192 + 512 * s);
-        }
-        if constexpr (VPAD) vmcnt_pad_n<w8::kEpiStores>(pyr);
-        if (late) __builtin_amdgcn_s_barrier();
-        for (int k = 0; k < nmax; ++k) {
-            f32x16 acc[8];
-            const int qn = qt + stride;
-            if (VPAD && k < nw) {
-                // both phases in one wave-uniform branch: every path that loads ring fragments issues
-                // the epilogue stores after them (vmcnt_pad_n, rmd_common.h)
-                if constexpr (ABL == 2 || ABL == 4) {
-#pragma unroll
-                    for (int ti = 0; ti < 8; ++ti)
-#pragma unroll
-                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
-                } else {
-                    bf16x8 a0[8], a1[8];
-                    w8::read_a8<0>(a0, smem, b0, b1);
-                    w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
-                                       gB + (size_t)min(qn, nqt - 1) * 8192);
-                }
-                __builtin_amdgcn_s_barrier();
-                if constexpr (ABL >= 4) {
-                    const pipe::Ctx ct = pipe::ctx_qtm(g, b, qt, rb, cb, pyr);
-                    const pipe::LaneOff lo = pipe::lane_offsets(ct, j, h, true);
-                    pipe::EpiState st;
-                    w8::epilogue<0, AUX>(acc, ct, lo, st);
-                } else {
-                    const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
-                    pipe::EpiState st;
-                    w8::epilogue<0, AUX>(acc, c, lo, st);
-                }
-                __builtin_amdgcn_s_barrier();
-                qt = qn;
-                continue;
-            }
-            if (!VPAD && k < nw) {
-                if constexpr (ABL == 2 || ABL == 4) {       // diagnostic: no k-loop (epilogue-only timing)
-#pragma unroll
-                    for (int ti = 0; ti < 8; ++ti)
-#pragma unroll
-                        for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
-                } else {
-                    bf16x8 a0[8], a1[8];
-                    w8::read_a8<0>(a0, smem, b0, b1);
-                    w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
-                                       gB + (size_t)min(qn, nqt - 1) * 8192);
-                }
-            }
-            __builtin_amdgcn_s_barrier();
-            if (!VPAD && k < nw) {
-                if constexpr (ABL >= 4) {       // diagnostic: query-tile-major store layout (timing only)
-                    const pipe::Ctx ct = pipe::ctx_qtm(g, b, qt, rb, cb, pyr);
-                    const pipe::LaneOff lo = pipe::lane_offsets(ct, j, h, true);
-                    pipe::EpiState st;
-                    w8::epilogue<0, AUX>(acc, ct, lo, st);
-                } else {
-                    const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
-                    pipe::EpiState st;
-                    w8::epilogue<0, AUX>(acc, c, lo, st);
-                }
-            }
-            __builtin_amdgcn_s_barrier();
-            qt = qn;
-        }
-        if (!late) __builtin_amdgcn_s_barrier();
-        return;
-    }
-    if (qt >= nqt) return;
-    if constexpr (RING) {
-        unsigned b0 = pb0, b1 = pb1;
-        asm volatile("" : "+v"(b0), "+v"(b1));
-        bf16x8 ring[w8::kRing];
+    // this workgroup's query tiles: [q_lo, q_hi) (all of them unless helpers split the block);
+    // waves 4-7 start one phase late; every wave runs 2 * nmax + 1 barriers
+    const int f0 = q_lo + split * WAVES;
+    int qt = f0 + w;
+    const int nmax = f0 < q_hi ? (q_hi - f0 + stride - 1) / stride : 0;
+    const int nw = qt < q_hi ? (q_hi - qt + stride - 1) / stride : 0;
+    const bool late = w >= 4;
+    unsigned b0 = pb0, b1 = pb1;
+    asm volatile("" : "+v"(b0), "+v"(b1));
+    bf16x8 ring[w8::kRing];
+    if (nw > 0) {
 #pragma unroll
         for (int s = 0; s < w8::kRing - 1; ++s) ring[s] = *reinterpret_cast<const bf16x8*>(gB + (size_t)qt * 8192 + 512 * s);
-        while (true) {
-            f32x16 acc[8];
-            const int qn = qt + stride;
+    }
+    vmcnt_pad_n<w8::kEpiStores>(pyr);
+    if (late) __builtin_amdgcn_s_barrier();
+    for (int k = 0; k < nmax; ++k) {
+        f32x16 acc[8];
+        const int qn = qt + stride;
+        if (k < nw) {
+            // both phases in one wave-uniform branch: every path that loads ring fragments issues
+            // the epilogue stores after them (vmcnt_pad_n, rmd_common.h)
             bf16x8 a0[8], a1[8];
             w8::read_a8<0>(a0, smem, b0, b1);
             w8::ksteps_ring<0>(acc, a0, a1, ring, smem, b0, b1, gB + (size_t)qt * 8192,
                                gB + (size_t)min(qn, nqt - 1) * 8192);
-            const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
+            __builtin_amdgcn_s_barrier();
+            const pipe::LaneOff lo = pipe::lane_offsets(c, qt * 32 + j, h);
             pipe::EpiState st;
             w8::epilogue<0, AUX>(acc, c, lo, st);
-            if (qn >= nqt) break;
+            __builtin_amdgcn_s_barrier();
             qt = qn;
+            continue;
         }
-        return;
-    }
-    bf16x8 bq[16];
-    {
-        const __bf16* p0 = gB + (size_t)qt * 8192;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(p0 + 512 * s);
-    }
-#ifdef RMD_DIAG
-    // A/B knobs: stagger % 1000 = s_sleep(16) count that desynchronises the two waves of each SIMD;
-    // stagger >= 1000 = static s_setprio 1 for the second-dispatched half (waves 4-7)
-    if ((stagger % 1000) && w >= 4)
-        for (int i = 0; i < stagger % 1000; ++i) __builtin_amdgcn_s_sleep(16);
-    if (stagger >= 1000 && w >= 4) __builtin_amdgcn_s_setprio(1);
-#else
-    (void)drop_stores;
-    (void)stagger;
-#endif
-    while (true) {
-        f32x16 acc[8];
-        const int qn = qt + stride;
-        // next tile's B fragments issue before this tile's stores, so waiting for them never
-        // waits for the stores (vmcnt counts in issue order)
-        const __bf16* pn = gB + (size_t)min(qn, nqt - 1) * 8192;
-        if constexpr (PAD) {
-            unsigned b0 = pb0, b1 = pb1;
-            asm volatile("" : "+v"(b0), "+v"(b1));     // two opaque bases: every other offset is an immediate
-            w8::mma_pad(acc, bq, smem, b0, b1);
-#pragma unroll
-            for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
-        } else if constexpr (ROLL) {
-            w8::mma(acc, bq, smem, lane_base, lane_c, pn);
-        } else {
-            w8::mma(acc, bq, smem, lane_base, lane_c);
-#pragma unroll
-            for (int s = 0; s < 16; ++s) bq[s] = *reinterpret_cast<const bf16x8*>(pn + 512 * s);
-        }
-        const pipe::LaneOff lo = pipe::lane_offsets(c, min(qt * 32 + j, N - 1), h, true);
-        pipe::EpiState st;
-        w8::epilogue<0, AUX>(acc, c, lo, st);
-        if (qn >= nqt) break;
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         qt = qn;
     }
+    if (!late) __builtin_amdgcn_s_barrier();
 }
 
 // GEMM path for a call: the w8 kernel needs bf16 operands, an fp16 pyramid, C <= 256 and 32-bit
-// store offsets (one wave's 16 level-0 rows < 1 GiB); larger maps (e.g. 4K frames) take the
-// stationary kernel (64-bit addressing), everything else the tiled kernel.  The diagnostic build
-// also honours RMD_GEMM_KERNEL = pipe | stationary | tiled.
-enum class Path { W8, PIPE, STATIONARY, TILED, X3 };
+// store offsets (one 16-row band of level 0 < 1 GiB); larger maps (e.g. 4K frames) take the
+// stationary kernel (64-bit addressing), everything else the tiled kernel.
+enum class Path { W8, STATIONARY, TILED, X3 };
+
+// query slots of the tiles layout for an H x W map (rmd.h)
+long long tiles_slots(int H, int W) {
+    return (long long)(H / 2) * ((W + 15) / 16) * 32 + ((H & 1) ? (long long)(W + 31) / 32 * 32 : 0);
+}
 
 Path gemm_path(const rmd_pyramid_desc& d, int C, int compute) {
     const int Cp = (C + kKC - 1) / kKC * kKC;
     if (compute == RMD_BF16X3) return x3::eligible(d, C) ? Path::X3 : Path::TILED;     // TILED: exact f32
     if (compute != RMD_BF16 || d.storage != RMD_F16 || Cp != 256) return Path::TILED;
-#ifdef RMD_DIAG
-    const char* k_env = getenv("RMD_GEMM_KERNEL");
-    if (k_env && strcmp(k_env, "tiled") == 0) return Path::TILED;
-    if (k_env && strcmp(k_env, "stationary") == 0) return Path::STATIONARY;
-    if (k_env && strcmp(k_env, "pipe") == 0) return Path::PIPE;
-#endif
-    const long long N = (long long)d.height * d.width;
-    const double span0 = 16.0 * d.tiles_x[0] * (double)N * 8 * 2;     // one wave's 16 level-0 rows (bytes)
+    const double slots = (double)tiles_slots(d.height, d.width);
+    const double span0 = 16.0 * ((d.width + 7) / 8 * 8) * slots * 2;   // one 16-row band of level 0 (bytes)
     if (span0 >= (double)(1u << 30)) return Path::STATIONARY;
     return Path::W8;
 }
+
+// the pyramid layout the GEMM of a call writes
+int path_layout(Path p) { return p == Path::W8 ? RMD_LAYOUT_TILES : RMD_LAYOUT_ROWS; }
 
 template <bool F32>
 int launch_prepare(const float* f1, const float* f2, int C, float scale, const rmd_pyramid_desc& d,
@@ -1437,10 +1038,12 @@ int launch_prepare(const float* f1, const float* f2, int C, float scale, const r
     const float prescale = F32 ? 1.0f : scale;
     if constexpr (!F32) {
         if (gemm_path(d, C, RMD_BF16) == Path::W8) {
-            const int nqt = (N + 31) / 32;
+            const int S = d.query_slots;
+            const int nqt = S / 32;
             const int lds = kPrepPx * kPrepStride;
+            const int nx = ((N > S ? N : S) + kPrepPx - 1) / kPrepPx;
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prep_pair), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-            prep_pair<<<dim3((N + kPrepPx - 1) / kPrepPx, d.batch, 2), 512, lds, st>>>(f1, f2, opA, opB, C, N, nqt, prescale);
+            prep_pair<<<dim3(nx, d.batch, 2), 512, lds, st>>>(f1, f2, opA, opB, C, d.height, d.width, S, nqt, prescale);
             return check_launch("rmd_corr_prepare");
         }
     }
@@ -1449,54 +1052,22 @@ int launch_prepare(const float* f1, const float* f2, int C, float scale, const r
     return check_launch("rmd_corr_prepare");
 }
 
-// Balanced schedule of the w8 GEMM (w8::Bal).  Costs in rounds (one query tile per wave, 8 per
-// workgroup): a primary with all tiles takes ceil(nqt/8); with helpers it takes ceil(qfull/8) and
-// the CUs left without a primary run ceil(nprim / spare) helpers of ceil((nqt-qfull)/8) + 0.2
-// rounds (the A re-staging).  qfull (a multiple of 8) minimises the larger of the two; helpers are
-// used only if that beats ceil(nqt/8).  Diagnostic knob RMD_W8_BAL: 0 off, 1 (product) pairing only,
-// 2 pairing + helpers.  Measured at cfg2 (profiles/gemm_ab_r02_bal.json): 0.2280 / 0.2257 / 0.2271 ms,
-// all bitwise identical — removing the 12.5 % of MFMA tiles that fall past the map and evening out
-// the per-CU work does not move the kernel: it is bound by the chip-wide pyramid write stream
-// (1.05 GB at 4.6-5.1 TB/s), not by any CU's share.  Pairing stays (the same time for 12.5 % fewer
-// MFMAs, 224 instead of 256 workgroups); helpers are off.
-w8::Bal w8_balance(const rmd_pyramid_desc& d, int qs, bool pp_kernel) {
-    const int N = d.height * d.width;
-    const int nqt = (N + 31) / 32;
+// Balanced schedule of the w8 GEMM (w8::Bal): the last block row is paired when it holds at most 8
+// target rows.  Measured at cfg2 (profiles/gemm_ab_r02_bal.json): 0.2280 (off) / 0.2257 (pairing) /
+// 0.2271 ms (pairing + one helper workgroup per primary running its tail query tiles on the CUs left
+// free), all bitwise identical — evening out the per-CU work does not move the kernel: it is bound by
+// the chip-wide pyramid write stream, not by any CU's share.  Pairing stays (the same time for 12.5 %
+// fewer MFMAs, 224 instead of 256 workgroups); the helper schedule is kept in the kernel (Bal) but not
+// used.
+w8::Bal w8_balance(const rmd_pyramid_desc& d, int qs) {
+    const int nqt = d.query_slots / 32;
     const int nrb = (d.height + 15) / 16, ncb = (d.width + 15) / 16;
     const int rows_last = d.height - 16 * (nrb - 1);
-    const int mode = pp_kernel ? env_knob("RMD_W8_BAL", 1) : 0;
     w8::Bal bal{0, nrb * ncb * d.batch * qs, nqt, 0};
-    if (mode == 0 || qs != 1) return bal;
+    if (qs != 1) return bal;
     if (nrb >= 2 && rows_last <= 8 && d.width % 32 == 0) {
         bal.pair = 1;
         bal.nprim = ((nrb - 1) * ncb + ncb / 2) * d.batch;
-    }
-    if (mode < 2) return bal;
-    static int ncu = 0;
-    if (ncu == 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-            ncu = n;
-        if (ncu <= 0) ncu = 256;
-    }
-    const int spare = ncu - bal.nprim;
-    if (spare <= 0 || bal.nprim % 8 != 0) return bal;
-    const int per = (bal.nprim + spare - 1) / spare;               // helpers per spare CU
-    double best = (double)((nqt + 7) / 8);
-    int qbest = nqt;
-    for (int qf = 8; qf < nqt; qf += 8) {
-        const double tp = (double)((qf + 7) / 8);
-        const double th = per * ((double)((nqt - qf + 7) / 8) + 0.2);
-        const double t = tp > th ? tp : th;
-        if (t < best - 0.25) {
-            best = t;
-            qbest = qf;
-        }
-    }
-    if (qbest < nqt) {
-        bal.helpers = 1;
-        bal.qfull = qbest;
     }
     return bal;
 }
@@ -1510,87 +1081,32 @@ int launch_pyramid(int C, float scale, const rmd_pyramid_desc& d, void* pyramid,
     T* opB = opA + (size_t)d.batch * N * Cp;
     const PyrGeom geom = make_geom(d);
     if constexpr (!F32 && sizeof(TOut) == 2) {
-        if (gemm_path(d, C, RMD_BF16) != Path::TILED) {
-            const int nblk = ((d.height + 15) / 16) * ((d.width + 15) / 16);
+        const Path path = gemm_path(d, C, RMD_BF16);
+        const int nblk = ((d.height + 15) / 16) * ((d.width + 15) / 16);
+        __half* out = reinterpret_cast<__half*>(pyramid);
+        if (path == Path::W8) {
+            // non-temporal pyramid stores (AUX = 2); query tiles split over workgroups only when the
+            // blocks alone do not fill the chip
+            const int nqt = d.query_slots / 32;
+            int qs = 1;
+            while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
+            auto kern = corr_pyramid_w8<2>;
+            const int lds_w8 = 256 * (int)w8::kPadRow;
+            const w8::Bal bal = w8_balance(d, qs);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds_w8);
+            kern<<<bal.nprim * (bal.helpers ? 2 : 1), 512, lds_w8, st>>>(opA, opB, geom, qs, out, bal);
+            return check_launch("rmd_corr_pyramid/gemm-w8");
+        }
+        if (path == Path::STATIONARY) {
             const int nqt = (N + 31) / 32;
             int qsplit = 1;
             while (nblk * d.batch * qsplit < 256 && qsplit * 16 <= nqt) qsplit *= 2;
             const int lds = 256 * Cp * 2;
             const int nwg = nblk * d.batch * qsplit;
-            __half* out = reinterpret_cast<__half*>(pyramid);
             __half* trash = reinterpret_cast<__half*>(opB + (size_t)d.batch * nqt * 32 * Cp);
-            const Path path = gemm_path(d, C, RMD_BF16);
-            if (path == Path::W8) {
-                // stores are non-temporal (aux bit 1, nt): measured 0.24 vs 0.26 ms plain at cfg2 (the
-                // pyramid is written once and read back a full GEMM later)
-                int qs = 1;
-                while (nblk * d.batch * qs < 256 && qs * 32 <= nqt) qs *= 2;
-                // product: padded LDS A block, B-fragment register ring, ping-pong MFMA / epilogue phases
-                auto kern = corr_pyramid_w8<2, false, true, true, true>;
-                int lds_w8 = 256 * (int)w8::kPadRow;
-                int drop = 0, stagger = 0;
-#ifdef RMD_DIAG
-                const int aux = env_knob("RMD_STORE_AUX", 2);
-                const bool roll = env_knob("RMD_W8_ROLL", 0) != 0;
-                if (env_knob("RMD_W8_PAD", 1) == 0) {      // previous XOR-swizzled layout
-                    kern = aux == 2 ? (roll ? corr_pyramid_w8<2, true, false> : corr_pyramid_w8<2, false, false>)
-                                    : (roll ? corr_pyramid_w8<0, true, false> : corr_pyramid_w8<0, false, false>);
-                    lds_w8 = lds;
-                } else if (env_knob("RMD_W8_RING", 2) == 2) {
-                    if (env_knob("RMD_ABLATE", 0) == 4) kern = corr_pyramid_w8<2, false, true, true, true, 4>;
-                    else if (env_knob("RMD_ABLATE", 0) == 5) kern = corr_pyramid_w8<2, false, true, true, true, 5>;
-                    else if (env_knob("RMD_ABLATE", 0) >= 2) kern = corr_pyramid_w8<2, false, true, true, true, 2>;
-                    else if (aux == 0) kern = corr_pyramid_w8<0, false, true, true, true>;
-                    // cache-policy A/B of the pyramid stores (gfx950 cpol bits: 1 sc0, 2 nt, 16 sc1)
-                    else if (aux == 1) kern = corr_pyramid_w8<1, false, true, true, true>;
-                    else if (aux == 3) kern = corr_pyramid_w8<3, false, true, true, true>;
-                    else if (aux == 16) kern = corr_pyramid_w8<16, false, true, true, true>;
-                    else if (aux == 17) kern = corr_pyramid_w8<17, false, true, true, true>;
-                    else if (aux == 18) kern = corr_pyramid_w8<18, false, true, true, true>;
-                    else if (aux == 19) kern = corr_pyramid_w8<19, false, true, true, true>;
-                    if (env_knob("RMD_W8_VPAD", 1) == 0 && env_knob("RMD_ABLATE", 0) == 0 && aux == 2)
-                        kern = corr_pyramid_w8<2, false, true, true, true, 0, false>;
-                } else if (env_knob("RMD_W8_RING", 2) == 1) {
-                    kern = corr_pyramid_w8<2, false, true, true>;
-                } else {
-                    kern = aux == 2 ? corr_pyramid_w8<2, false, true> : corr_pyramid_w8<0, false, true>;
-                }
-                drop = env_knob("RMD_ABLATE", 0) == 1 || env_knob("RMD_ABLATE", 0) == 3;
-                stagger = env_knob("RMD_W8_STAGGER", 0);
-#endif
-                bool pp_kernel = true;
-#ifdef RMD_DIAG
-                pp_kernel = env_knob("RMD_W8_PAD", 1) != 0 && env_knob("RMD_W8_RING", 2) == 2;
-#endif
-                const w8::Bal bal = w8_balance(d, qs, pp_kernel);
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds_w8);
-                kern<<<bal.nprim * (bal.helpers ? 2 : 1), 512, lds_w8, st>>>(opA, opB, geom, qs, out, drop, stagger, bal);
-                return check_launch("rmd_corr_pyramid/gemm-w8");
-            }
-#ifdef RMD_DIAG
-            if (path == Path::PIPE) {
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_pipe),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-                corr_pyramid_pipe<<<nwg, 256, lds, st>>>(opA, opB, geom, qsplit, out, env_knob("RMD_ABLATE", 0) == 1);
-                return check_launch("rmd_corr_pyramid/gemm-pipe");
-            }
-            const int abl = env_knob("RMD_ABLATE", 0);
-            const int th = env_knob("RMD_GEMM_WAVES", 4) == 8 ? 1 : 2;     // 4 (default) or 8 waves
-            switch (th * 4 + (abl >= 0 && abl <= 2 ? abl : 0)) {
-#define RMD_SCASE(TH, ABL)                                                                                      \
-    case TH * 4 + ABL:                                                                                          \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<TH, ABL>),              \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);                             \
-        corr_pyramid_stationary<TH, ABL><<<nwg, STraits<TH>::kThreads, lds, st>>>(opA, opB, geom, qsplit, out, trash); \
-        break;
-                RMD_SCASE(1, 0) RMD_SCASE(1, 1) RMD_SCASE(1, 2) RMD_SCASE(2, 0) RMD_SCASE(2, 1) RMD_SCASE(2, 2)
-#undef RMD_SCASE
-            }
-#else
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(corr_pyramid_stationary<2, 0>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             corr_pyramid_stationary<2, 0><<<nwg, STraits<2>::kThreads, lds, st>>>(opA, opB, geom, qsplit, out, trash);
-#endif
             return check_launch("rmd_corr_pyramid/gemm-stationary");
         }
     }
@@ -1609,11 +1125,24 @@ int check_args(const rmd_pyramid_desc* d, int channels, int compute) {
     RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16 || compute == RMD_BF16X3, RMD_ERR_ARG,
                 "rmd_corr_pyramid: compute must be F32, BF16 or BF16X3");
     RMD_REQUIRE(d->storage == RMD_F32 || d->storage == RMD_F16, RMD_ERR_ARG, "rmd_corr_pyramid: storage must be F32 or F16");
+    const int want = path_layout(gemm_path(*d, channels, compute));
+    RMD_REQUIRE(d->layout == want, RMD_ERR_ARG,
+                "rmd_corr_pyramid: the %s GEMM writes layout %d, desc has layout %d (describe with rmd_pyramid_describe_for)",
+                want == RMD_LAYOUT_TILES ? "w8" : "selected", want, d->layout);
     return RMD_OK;
 }
 
 }  // namespace
 }  // namespace rmd
+
+extern "C" int rmd_pyramid_describe_for(int batch, int height, int width, int levels, int storage, int channels,
+                                        int compute, rmd_pyramid_desc* d) {
+    int rc = rmd_pyramid_describe_layout(batch, height, width, levels, storage, RMD_LAYOUT_ROWS, d);
+    if (rc || channels <= 0) return rc;
+    if (rmd::gemm_path(*d, channels, compute) == rmd::Path::W8)
+        rc = rmd_pyramid_describe_layout(batch, height, width, levels, storage, RMD_LAYOUT_TILES, d);
+    return rc;
+}
 
 extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, int channels, int compute) {
     if (!d || channels <= 0) return 0;
@@ -1623,15 +1152,16 @@ extern "C" size_t rmd_corr_pyramid_workspace_bytes(const rmd_pyramid_desc* d, in
     }
     const size_t Cp = (size_t)(channels + rmd::kKC - 1) / rmd::kKC * rmd::kKC;
     const size_t es = compute == RMD_F32 ? 4 : 2;
-    const size_t N = (size_t)d->height * d->width, Npad = (N + 31) / 32 * 32;   // B operand padded to 32-query tiles
-    return (size_t)d->batch * (N + Npad) * Cp * es + 32 * 1024;                  // + trash slots (<= 32 x 1 KiB)
+    const size_t N = (size_t)d->height * d->width;
+    const size_t S = d->query_slots > 0 && (size_t)d->query_slots > N ? (size_t)d->query_slots : N;
+    const size_t Npad = (S + 31) / 32 * 32;                         // B operand padded to 32-query tiles
+    return (size_t)d->batch * (N + Npad) * Cp * es + 32 * 1024;     // + trash slots (<= 32 x 1 KiB)
 }
 
 extern "C" const char* rmd_corr_gemm_kernel(const rmd_pyramid_desc* d, int channels, int compute) {
-    if (rmd::check_args(d, channels, compute) != RMD_OK) return "invalid";
+    if (!d || channels <= 0) return "invalid";
     switch (rmd::gemm_path(*d, channels, compute)) {
         case rmd::Path::W8: return "w8";
-        case rmd::Path::PIPE: return "pipe";
         case rmd::Path::STATIONARY: return "stationary";
         case rmd::Path::X3: return "x3";
         default: return "tiled";

@@ -42,6 +42,8 @@ struct PyrGeom {
     int th[RMD_MAX_LEVELS], tw[RMD_MAX_LEVELS];
     int ty[RMD_MAX_LEVELS], tx[RMD_MAX_LEVELS];
     long long off[RMD_MAX_LEVELS];
+    int layout;       // RMD_LAYOUT_ROWS / RMD_LAYOUT_TILES
+    int slots;        // query slots per chunk position (H*W in the row layout)
 };
 
 inline PyrGeom make_geom(const rmd_pyramid_desc& d) {
@@ -59,7 +61,31 @@ inline PyrGeom make_geom(const rmd_pyramid_desc& d) {
         g.tx[l] = d.tiles_x[l];
         g.off[l] = d.level_offset[l];
     }
+    g.layout = d.layout;
+    g.slots = d.query_slots;
     return g;
+}
+
+// Query slots of the tiles layout (rmd.h RMD_LAYOUT_TILES): 2 x 16 query tiles of 32 slots whose
+// 8-slot groups are 2 x 4 query patches, row pairs in order, an odd last row in raster order.
+__host__ __device__ __forceinline__ int tiles_slot(int y1, int x1, int H, int W) {
+    const int qx = (W + 15) >> 4, hp = H >> 1;
+    if (y1 < 2 * hp)
+        return (((y1 >> 1) * qx + (x1 >> 4)) << 5) + (((x1 & 15) >> 2) << 3) + ((y1 & 1) << 2) + (x1 & 3);
+    return hp * qx * 32 + x1;
+}
+
+// pixel of slot s (x1 >= W or y1 >= H: a padding slot)
+__host__ __device__ __forceinline__ void tiles_pixel(int s, int H, int W, int& y1, int& x1) {
+    const int qx = (W + 15) >> 4, hp = H >> 1, base = hp * qx * 32;
+    if (s < base) {
+        const int t = s >> 5, j = s & 31;
+        y1 = 2 * (t / qx) + ((j >> 2) & 1);
+        x1 = 16 * (t % qx) + ((j >> 3) << 2) + (j & 3);
+    } else {
+        y1 = (H & 1) ? H - 1 : H;
+        x1 = s - base;
+    }
 }
 
 // row-chunk width of level l: 8, 8, 4, 2 elements — the 16 target columns of a GEMM workgroup

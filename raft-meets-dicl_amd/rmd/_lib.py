@@ -12,6 +12,7 @@ import torch  # noqa: F401  (load torch's libamdhip64 first so librmd.so binds t
 
 RMD_OK = 0
 RMD_F32, RMD_F16, RMD_BF16, RMD_BF16X3 = 0, 1, 2, 3
+RMD_LAYOUT_ROWS, RMD_LAYOUT_TILES = 0, 1
 MAX_LEVELS = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -29,6 +30,7 @@ class PyramidDesc(ctypes.Structure):
         ("tiles_y", ctypes.c_int * MAX_LEVELS), ("tiles_x", ctypes.c_int * MAX_LEVELS),
         ("level_offset", ctypes.c_longlong * MAX_LEVELS),
         ("total_elements", ctypes.c_longlong),
+        ("layout", ctypes.c_int), ("query_slots", ctypes.c_int),
     ]
 
 
@@ -43,6 +45,8 @@ _I = ctypes.c_int
 _U = ctypes.c_uint
 _SIGS = {
     "rmd_pyramid_describe": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(PyramidDesc)]),
+    "rmd_pyramid_describe_layout": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(PyramidDesc)]),
+    "rmd_pyramid_describe_for": (_I, [_I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(PyramidDesc)]),
     "rmd_corr_pyramid_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(PyramidDesc), _I, _I]),
     "rmd_corr_pyramid": (_I, [_P, _P, _I, ctypes.c_float, ctypes.POINTER(PyramidDesc), _I, _P, _P, _P]),
     "rmd_corr_lookup": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
@@ -115,10 +119,18 @@ def check(rc, what):
         raise RmdError(f"{what} failed (code {rc}): {msg}")
 
 
-def describe(batch, height, width, levels, storage):
+def describe(batch, height, width, levels, storage, layout=RMD_LAYOUT_ROWS):
     d = PyramidDesc()
-    check(lib().rmd_pyramid_describe(batch, height, width, levels, storage, ctypes.byref(d)),
+    check(lib().rmd_pyramid_describe_layout(batch, height, width, levels, storage, layout, ctypes.byref(d)),
           "rmd_pyramid_describe")
+    return d
+
+
+def describe_for(batch, height, width, levels, storage, channels, compute):
+    """The pyramid rmd_corr_pyramid writes for (channels, compute): tiles layout on the w8 GEMM."""
+    d = PyramidDesc()
+    check(lib().rmd_pyramid_describe_for(batch, height, width, levels, storage, channels, compute, ctypes.byref(d)),
+          "rmd_pyramid_describe_for")
     return d
 
 

@@ -7,7 +7,7 @@ and, where the reference's module is trained through it, an autograd formula who
 an rmd operator.  Schemas follow SURVEY.md §8(b):
 
   corr_pyramid(fmap1, fmap2, levels, compute, storage, scale) -> pyramid     raft.py:18-47
-  corr_lookup(pyramid, coords, levels, radius, level_mask) -> corr           raft.py:49-95
+  corr_lookup(pyramid, coords, levels, radius, level_mask, layout) -> corr   raft.py:49-95
   corr_otf_prepare / corr_otf_lookup                                        raft_fs.py:13-87, corr/dot.py:25-57
   dicl_stack(fmap1, fmap2, coords, radius, level, norm_h, norm_w, extra) ->  corr/dicl.py:26-54,
         (B, 2r+1, 2r+1, 2C[+2], h, w)                                        dicl_emb.py:51-89, raft_dicl_ml.py:294-315
@@ -35,7 +35,8 @@ LIB = torch.library.Library("rmd", "DEF")
 
 _SCHEMAS = {
     "corr_pyramid": "corr_pyramid(Tensor fmap1, Tensor fmap2, int levels, int compute, int storage, float scale) -> Tensor",
-    "corr_lookup": "corr_lookup(Tensor pyramid, Tensor coords, int levels, int radius, int level_mask) -> Tensor",
+    "corr_lookup": ("corr_lookup(Tensor pyramid, Tensor coords, int levels, int radius, int level_mask, int layout) "
+                    "-> Tensor"),
     "corr_otf_prepare": "corr_otf_prepare(Tensor fmap1, Tensor fmap2, int levels, int compute, float scale) -> Tensor",
     "corr_otf_lookup": ("corr_otf_lookup(Tensor workspace, Tensor coords, int channels, int levels, int compute, "
                         "int radius, int level_mask) -> Tensor"),
@@ -109,12 +110,21 @@ def _f32(t):
 _DESC = {}
 
 
-def describe(batch, height, width, levels, storage):
-    """rmd_pyramid_describe, cached per geometry (host-only)."""
-    key = (batch, height, width, levels, storage)
+def describe(batch, height, width, levels, storage, layout=_lib.RMD_LAYOUT_ROWS):
+    """rmd_pyramid_describe_layout, cached per geometry (host-only)."""
+    key = (batch, height, width, levels, storage, layout)
     d = _DESC.get(key)
     if d is None:
-        d = _DESC[key] = _lib.describe(batch, height, width, levels, storage)
+        d = _DESC[key] = _lib.describe(batch, height, width, levels, storage, layout)
+    return d
+
+
+def describe_for(batch, height, width, levels, storage, channels, compute):
+    """rmd_pyramid_describe_for: the layout the GEMM of (channels, compute) writes, cached."""
+    key = ("for", batch, height, width, levels, storage, channels, compute)
+    d = _DESC.get(key)
+    if d is None:
+        d = _DESC[key] = _lib.describe_for(batch, height, width, levels, storage, channels, compute)
     return d
 
 
@@ -134,7 +144,7 @@ def _corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
     _check_fmaps(fmap1, fmap2)
     f1, f2 = _f32(fmap1), _f32(fmap2)
     b, c, h, w = f1.shape
-    d = describe(b, h, w, levels, storage)
+    d = describe_for(b, h, w, levels, storage, c, compute)
     lib = _lib.lib()
     ws = torch.empty(lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), c, compute), dtype=torch.uint8,
                      device=f1.device)
@@ -148,8 +158,8 @@ def _corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
 @_fake("corr_pyramid")
 def _(fmap1, fmap2, levels, compute, storage, scale):
     _check_fmaps(fmap1, fmap2)
-    b, _, h, w = fmap1.shape
-    return fmap1.new_empty((describe(b, h, w, levels, storage).total_elements,), dtype=_STORAGE[storage])
+    b, c, h, w = fmap1.shape
+    return fmap1.new_empty((describe_for(b, h, w, levels, storage, c, compute).total_elements,), dtype=_STORAGE[storage])
 
 
 def _lookup_out(pyramid, coords, levels, radius):
@@ -165,13 +175,13 @@ def _check_device(name, *ts):
 
 
 @_cuda("corr_lookup")
-def _corr_lookup(pyramid, coords, levels, radius, level_mask):
+def _corr_lookup(pyramid, coords, levels, radius, level_mask, layout):
     b, two, h, w = coords.shape
     if pyramid.dtype not in _STORAGE_CODE or pyramid.dim() != 1 or not pyramid.is_contiguous():
         raise ValueError(f"corr_lookup: pyramid must be a contiguous 1-D float32/float16 tensor, got "
                          f"{pyramid.dtype} {tuple(pyramid.shape)}")
     _check_device("corr_lookup", pyramid, coords)
-    d = describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype])
+    d = describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype], layout)
     if two != 2 or pyramid.numel() != d.total_elements:
         raise ValueError(f"corr_lookup: coords {tuple(coords.shape)} do not match the pyramid ({pyramid.numel()} elements)")
     co = _f32(coords)
@@ -183,7 +193,7 @@ def _corr_lookup(pyramid, coords, levels, radius, level_mask):
 
 
 @_fake("corr_lookup")
-def _(pyramid, coords, levels, radius, level_mask):
+def _(pyramid, coords, levels, radius, level_mask, layout):
     return _lookup_out(pyramid, coords, levels, radius)
 
 

@@ -65,13 +65,24 @@ class Pyramid:
         """Level i in the reference layout (B, H, W, 1, H_i, W_i) as float32 — for tests/debugging."""
         d = self.desc
         b, h, w = d.batch, d.height, d.width
-        cw, nc = d.tile_w[i], d.tiles_x[i]
+        th, tw, ty, tx = d.tile_h[i], d.tile_w[i], d.tiles_y[i], d.tiles_x[i]
         hl, wl = d.level_h[i], d.level_w[i]
-        n = h * w
+        s = d.query_slots
         off = d.level_offset[i]
-        x = self.data[off: off + b * hl * nc * n * cw].view(b, hl, nc, n, cw)
-        x = x.permute(0, 3, 1, 2, 4).reshape(b, n, hl, nc * cw)[..., :wl]
+        x = self.data[off: off + b * ty * tx * s * th * tw].view(b, ty, tx, s, th, tw)
+        x = x.permute(0, 3, 1, 4, 2, 5).reshape(b, s, ty * th, tx * tw)[..., :hl, :wl]
+        if d.layout == _lib.RMD_LAYOUT_TILES:
+            x = x.index_select(1, torch.as_tensor(tiles_slots(h, w), device=x.device))
         return x.float().reshape(b, h, w, 1, hl, wl)
+
+
+def tiles_slots(h, w):
+    """Query slot of every pixel (raster order) in the tiles layout (include/rmd.h RMD_LAYOUT_TILES)."""
+    y1, x1 = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    qx, hp = (w + 15) // 16, h // 2
+    s = ((y1 // 2) * qx + x1 // 16) * 32 + ((x1 % 16) // 4) * 8 + (y1 % 2) * 4 + x1 % 4
+    s = torch.where(y1 < 2 * hp, s, hp * qx * 32 + x1)
+    return s.reshape(-1)
 
 
 def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None):
@@ -89,7 +100,7 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     compute, storage = PRECISIONS[precision or get_default_precision()]
     b, c, h, w = fmap1.shape
     scale = 1.0 / float(c) ** 0.5 if scale is None else float(scale)
-    d = library.describe(b, h, w, levels, storage)
+    d = library.describe_for(b, h, w, levels, storage, c, compute)
     if events is None:
         return Pyramid(torch.ops.rmd.corr_pyramid(fmap1, fmap2, levels, compute, storage, scale), d, c, scale)
     f1 = fmap1.detach().float().contiguous()
@@ -117,7 +128,7 @@ def corr_lookup(pyr, coords, radius, mask_costs=()):
     d = pyr.desc
     if tuple(coords.shape) != (d.batch, 2, d.height, d.width):
         raise ValueError(f"coords must be (B,2,H,W)=({d.batch},2,{d.height},{d.width}), got {tuple(coords.shape)}")
-    return torch.ops.rmd.corr_lookup(pyr.data, coords, d.levels, radius, _mask_bits(mask_costs, d.levels))
+    return torch.ops.rmd.corr_lookup(pyr.data, coords, d.levels, radius, _mask_bits(mask_costs, d.levels), d.layout)
 
 
 # ---- on-the-fly lookup (raft_fs semantics without the volume) -------------------------------------

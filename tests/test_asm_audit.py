@@ -114,8 +114,8 @@ def test_every_asm_load_window_is_exact(kernel_asm):
 
 @pytest.fixture
 def w8_asm(module_asm):
-    m = re.search(r"^(_ZN3rmd\w*corr_pyramid_w8ILi2ELb0E\w*):[^\n]*\n(.*?)\.end_amdhsa_kernel", module_asm, re.S | re.M)
-    assert m, "corr_pyramid_w8<2, false> not found"
+    m = re.search(r"^(_ZN3rmd\w*corr_pyramid_w8ILi2E\w*):[^\n]*\n(.*?)\.end_amdhsa_kernel", module_asm, re.S | re.M)
+    assert m, "corr_pyramid_w8<2> not found"
     return m.group(2).split("\n")
 
 

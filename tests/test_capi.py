@@ -4,6 +4,7 @@ and the host-only geometry call behaves (no compute calls without a GPU)."""
 import os
 import re
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -44,6 +45,42 @@ def test_describe_cfg2_geometry():
     sizes = [55 * 128, 27 * 64, 13 * 32, 6 * 16]
     assert d.total_elements == 8 * n * sum(sizes)
     assert [d.level_offset[i] for i in range(4)] == [0] + [8 * n * sum(sizes[:i]) for i in range(1, 4)]
+
+
+def test_describe_for_w8_tiles_layout_geometry():
+    """The w8 GEMM (bf16 compute, fp16 storage, C = 256) writes the tiles layout (include/rmd.h):
+    2x4, 2x4, 1x4, 1x2 chunks and 2 x 16 query tiles; cfg2's odd H = 55 puts its last row in raster
+    slots, so query_slots == H*W."""
+    from rmd import _lib
+    d = _lib.describe_for(8, 55, 128, 4, _lib.RMD_F16, 256, _lib.RMD_BF16)
+    assert d.layout == _lib.RMD_LAYOUT_TILES and d.query_slots == 27 * 8 * 32 + 128 == 55 * 128
+    assert [d.tile_h[i] for i in range(4)] == [2, 2, 1, 1]
+    assert [d.tile_w[i] for i in range(4)] == [4, 4, 4, 2]
+    assert [d.tiles_y[i] for i in range(4)] == [28, 14, 13, 6]
+    assert [d.tiles_x[i] for i in range(4)] == [32, 16, 8, 8]
+    sizes = [28 * 2 * 128, 14 * 2 * 64, 13 * 32, 6 * 16]
+    assert d.total_elements == 8 * d.query_slots * sum(sizes)
+    # every other GEMM keeps the row layout
+    for storage, compute, c in ((_lib.RMD_F32, _lib.RMD_BF16X3, 256), (_lib.RMD_F16, _lib.RMD_BF16, 128),
+                                (_lib.RMD_F32, _lib.RMD_F32, 256)):
+        assert _lib.describe_for(8, 55, 128, 4, storage, c, compute).layout == _lib.RMD_LAYOUT_ROWS
+    with pytest.raises(_lib.RmdError):
+        _lib.describe(1, 8, 8, 2, _lib.RMD_F32, _lib.RMD_LAYOUT_TILES)     # tiles are fp16 only
+
+
+@pytest.mark.parametrize("h,w", [(55, 128), (46, 62), (9, 17), (1, 40), (48, 160)])
+def test_tiles_slots_are_a_padded_bijection(h, w):
+    """rmd.ops.tiles_slots (the unpack map) is injective, stays below query_slots, and every 8-slot
+    group is a 2 x 4 query patch (or 8 consecutive pixels of an odd last row)."""
+    from rmd import _lib, ops
+    s = ops.tiles_slots(h, w).numpy()
+    d = _lib.describe(1, h, w, 1, _lib.RMD_F16, _lib.RMD_LAYOUT_TILES)
+    assert len(set(s.tolist())) == h * w and s.max() < d.query_slots and d.query_slots % 32 == 0
+    y1, x1 = np.divmod(np.arange(h * w), w)
+    for g in np.unique(s // 8):
+        m = s // 8 == g
+        dy, dx = np.ptp(y1[m]), np.ptp(x1[m])
+        assert (dy <= 1 and dx <= 3) or (dy == 0 and dx <= 7 and (h % 2 == 1) and y1[m][0] == h - 1)
 
 
 @pytest.mark.parametrize("args", [(0, 4, 4, 1, 0), (1, 4, 4, 5, 0), (1, 4, 4, 1, 7), (1, 7, 9, 4, 0)])

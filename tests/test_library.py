@@ -29,9 +29,10 @@ def test_fake_kernels_propagate_shapes():
     with FakeTensorMode():
         f1 = torch.empty(2, 256, 55, 128, device="cuda")
         pyr = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16, _lib.RMD_F16, 0.0625)
-        assert pyr.dtype == torch.float16 and pyr.numel() == _lib.describe(2, 55, 128, 4, _lib.RMD_F16).total_elements
+        d = _lib.describe(2, 55, 128, 4, _lib.RMD_F16, _lib.RMD_LAYOUT_TILES)     # the w8 GEMM's layout
+        assert pyr.dtype == torch.float16 and pyr.numel() == d.total_elements
         co = torch.empty(2, 2, 55, 128, device="cuda")
-        assert torch.ops.rmd.corr_lookup(pyr, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        assert torch.ops.rmd.corr_lookup(pyr, co, 4, 4, 0, d.layout).shape == (2, 324, 55, 128)
         f = torch.empty(2, 32, 12, 16, device="cuda")
         c2 = torch.empty(2, 2, 12, 16, device="cuda")
         assert torch.ops.rmd.dicl_stack(f, f, c2, 4, 0, 12, 16, False).shape == (2, 9, 9, 64, 12, 16)
@@ -72,7 +73,7 @@ def test_opcheck_operator_families():
     for op, args in cases:
         torch.library.opcheck(op, args, test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
     pyr = torch.ops.rmd.corr_pyramid(f1.detach(), f2.detach(), 3, _lib.RMD_BF16X3, _lib.RMD_F32, 0.25)
-    torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0),
+    torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0, _lib.RMD_LAYOUT_ROWS),
                           test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
 
 
