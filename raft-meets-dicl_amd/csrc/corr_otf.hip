@@ -18,8 +18,8 @@
 // relative; same split as the fp32-mode GEMM), in the workspace bytes of f32 operands.  RMD_F32 keeps
 // the exact f32 MFMA (fp32-exact).
 //
-// Lookup: one 256-thread block per (16 x 2 query block, batch), looping over the levels.  The 32 queries' (2r+2)^2
-// integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
+// Lookup: one 256-thread block per (query block of 16 x 1 (bf16) / 16 x 2 (fp32 modes) pixels, batch),
+// looping over the levels.  The block's queries' (2r+2)^2 integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
 // processed in bands of whole rows of at most kMaxT targets: S = band targets x queries, one 16x16
 // MFMA tile per (target segment, query segment), into LDS.  Each (query, x-offset) thread keeps its
 // window rows x-interpolated in registers across bands and finally y-interpolates exactly as
@@ -35,15 +35,37 @@ namespace {
 
 constexpr int kThreads = 256;                        // prepare kernels
 constexpr int kLookThreads = 256, kWaves = kLookThreads / 64;
-constexpr int kBX = 16, kBY = 2, kQ = kBX * kBY;     // query block = 2 query segments
-#ifndef RMD_OTF_MAXT
-#define RMD_OTF_MAXT 384
-#endif
-constexpr int kMaxT = RMD_OTF_MAXT;                  // targets of one band
+constexpr int kMaxT = 384;                           // targets of one band
 constexpr int kLd = kMaxT + 5;                       // S row stride (spreads queries over banks)
-// diagnostic variant (RMD_OTF_PF=1): the next band task's target fragments in flight during this task's
-// MFMAs; needs 256 VGPRs (2 waves/SIMD, spills) and measured slower: 123 vs 100 us at cfg2 bf16
-// (profiles/otf_ablate_r02.json)
+// Query block and occupancy per compute (-D knobs for A/B builds, tools/_gpu_r03c.sh).  cfg2, one box
+// (profiles/otf_block_ab_r03.json): bf16 16x1 blocks at 2 workgroups per CU 90 us vs 16x2 at one 112 us
+// (16x4: 147, 32x1: 103 — larger boxes waste MFMA tiles and cut the number of blocks in flight; the
+// kernel is latency-bound at ~13 % of the MFMA rate it issues); split-bf16 16x2 at 2 per CU 203 vs
+// 214 us (16x1: 211).
+#ifndef RMD_OTF_QSX_B
+#define RMD_OTF_QSX_B 1
+#endif
+#ifndef RMD_OTF_QSY_B
+#define RMD_OTF_QSY_B 1
+#endif
+#ifndef RMD_OTF_QSX_X
+#define RMD_OTF_QSX_X 1
+#endif
+#ifndef RMD_OTF_QSY_X
+#define RMD_OTF_QSY_X 2
+#endif
+#ifndef RMD_OTF_OCC_B
+#define RMD_OTF_OCC_B 2
+#endif
+#ifndef RMD_OTF_OCC_X
+#define RMD_OTF_OCC_X 2
+#endif
+#ifndef RMD_OTF_QSX_X
+#define RMD_OTF_QSX_X 1
+#endif
+#ifndef RMD_OTF_QSY_X
+#define RMD_OTF_QSY_X 2
+#endif
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -210,16 +232,26 @@ __device__ __forceinline__ void seg_mma(f32x4& acc, const typename Seg<T>::frag*
     }
 }
 
+// Query block = QSX x QSY query segments (16 x 1 pixels each): 16 QSX x QSY queries.  Larger blocks
+// load each target segment of their box once for more queries (the L2 -> CU operand traffic is the
+// bound: every block re-reads its box), at the cost of MFMA tiles for targets outside a query's own
+// window.  A 16 x 4 block (bf16) reads 2.5x fewer target bytes per query than 16 x 2.
+template <int QSX, int QSY> struct QBlock {
+    static constexpr int kQS = QSX * QSY, kBX = 16 * QSX, kBY = QSY, kQ = kBX * kBY;
+};
+
 // 1-D grid over (batch, query block), XCD-aware: adjacent query blocks, whose target boxes overlap,
-// run on the same XCD and share its L2.  One block runs every level of its 32 queries, so the query
+// run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, bool PF>
-__global__ void __launch_bounds__(kLookThreads, PF ? 2 : 1)
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC>
+__global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
-                  const float* __restrict__ coords, unsigned zmask, float* __restrict__ out, int ablate) {
+                  const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
     using SG = Seg<T>;
     using frag = typename SG::frag;
+    using QB = QBlock<QSX, QSY>;
+    constexpr int kQS = QB::kQS, kBX = QB::kBX, kBY = QB::kBY, kQ = QB::kQ;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K;
     extern __shared__ float S[];                       // [kQ][kLd]: band (boxed) or patch (per query)
     // every level's window origins / fractions and the block's bounding box per level, computed once
@@ -239,46 +271,42 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     const int cp = CPT > 0 ? CPT : g.Cp;
     const int nls = cp / SG::LSC;
     const size_t segsz = (size_t)16 * cp * NP;
-    const T* qsb = qseg + ((size_t)b * g.QS + (size_t)qy0 * g.qnsx + (qx0 >> 4)) * segsz;
-    const T* qsb1 = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + 1, g.H - 1) * g.qnsx + (qx0 >> 4)) * segsz;
+    // query segment s = (row sy, column sx) of the block: its operand rows (clamped at the map edge)
+    const T* qsb[kQS];
+#pragma unroll
+    for (int s = 0; s < kQS; ++s)
+        qsb[s] = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + s / QSX, g.H - 1) * g.qnsx +
+                         min((qx0 >> 4) + s % QSX, g.qnsx - 1)) * segsz;
 
-    // the block's two query segments (CPT > 0): one coalesced copy into LDS, overlapping the coords
+    // the block's query segments (CPT > 0): one coalesced copy into LDS, overlapping the coords
     // load; each wave then keeps its register fragments for every level and target segment
     constexpr int NLS = CPT > 0 ? CPT / SG::LSC * NP : 1;                 // load steps per segment
     constexpr int QV = CPT > 0 ? 16 * CPT * NP * (int)sizeof(T) / 16 : 0;     // 16-B vectors per segment
-    static_assert(2 * QV * 16 <= kQ * kLd * 4, "two query segments must fit the S buffer");
+    static_assert(kQS * QV * 16 <= kQ * kLd * 4, "the query segments must fit the S buffer");
     if constexpr (CPT > 0) {
-        const uint4* s0 = reinterpret_cast<const uint4*>(qsb);
-        const uint4* s1 = reinterpret_cast<const uint4*>(qsb1);
         uint4* dst = reinterpret_cast<uint4*>(S);
-        for (int v = tid; v < QV; v += kLookThreads) {
-            dst[v] = s0[v];
-            dst[QV + v] = s1[v];
+#pragma unroll
+        for (int s = 0; s < kQS; ++s) {
+            const uint4* src = reinterpret_cast<const uint4*>(qsb[s]);
+            for (int v = tid; v < QV; v += kLookThreads) dst[s * QV + v] = src[v];
         }
     }
-    // thread (level tid / kQ, query tid % kQ)
-    float cx0 = 0.f, cy0 = 0.f;
-    if (tid < kQ * g.L) {
-        const int q = tid % kQ;
-        const int y = min(qy0 + q / kBX, g.H - 1), x = min(qx0 + q % kBX, g.W - 1);
-        cx0 = coords[((size_t)b * 2 + 0) * N + y * g.W + x];
-        cy0 = coords[((size_t)b * 2 + 1) * N + y * g.W + x];
-    }
-    static_assert(kQ * RMD_MAX_LEVELS <= kLookThreads, "one thread per (level, query)");
     if (tid < RMD_MAX_LEVELS * 4) box[tid >> 2][tid & 3] = (tid & 1) ? -(1 << 30) : (1 << 30);
     __syncthreads();
-    frag q0[NLS], q1[NLS];
+    frag qf[kQS][NLS];
     if constexpr (CPT > 0) {
         const frag* qs = reinterpret_cast<const frag*>(S);
 #pragma unroll
-        for (int ls = 0; ls < NLS; ++ls) {
-            q0[ls] = qs[ls * 64 + lane];
-            q1[ls] = qs[(NLS + ls) * 64 + lane];
-        }
+        for (int s = 0; s < kQS; ++s)
+#pragma unroll
+            for (int ls = 0; ls < NLS; ++ls) qf[s][ls] = qs[(s * NLS + ls) * 64 + lane];
     }
-    if (tid < kQ * g.L) {
-        // query's window origin at level L (coords clamped as rmd_corr_lookup does)
-        const int q = tid % kQ, L = tid / kQ;
+    // thread (level, query) items: every level's window origin (coords clamped as rmd_corr_lookup does)
+    for (int it = tid; it < kQ * g.L; it += kLookThreads) {
+        const int q = it % kQ, L = it / kQ;
+        const int y = min(qy0 + q / kBX, g.H - 1), x = min(qx0 + q % kBX, g.W - 1);
+        const float cx0 = coords[((size_t)b * 2 + 0) * N + y * g.W + x];
+        const float cy0 = coords[((size_t)b * 2 + 1) * N + y * g.W + x];
         const float inv = 1.0f / (float)(1 << L);
         const float rx = cx0 * inv, ry = cy0 * inv;
         const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f);
@@ -329,59 +357,50 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             for (int ry0 = by0; ry0 < by0 + th; ry0 += bh) {
                 const int nrow = min(bh, by0 + th - ry0), ntask = nrow * nseg;
                 // C[target 4*(lane>>4)+e][query lane&15] -> S[query][band target]
-                auto store = [&](const f32x4& a0, const f32x4& a1, int task) {
+                auto store = [&](const f32x4& a, int s, int task) {
                     const int col = (task / nseg) * sw + (task % nseg) * 16 + 4 * (lane >> 4), j = lane & 15;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        S[j * kLd + col + e] = a0[e];
-                        S[(16 + j) * kLd + col + e] = a1[e];
-                    }
+                    for (int e = 0; e < 4; ++e) S[(s * 16 + j) * kLd + col + e] = a[e];
                 };
                 auto tptr = [&](int task) {
                     return tlev + ((size_t)(ry0 + task / nseg) * g.nsx[L] + sa + task % nseg) * segsz +
                            (size_t)lane * SG::LE;
                 };
                 if constexpr (CPT > 0) {
-                    // the next task's target fragments load while this task's MFMAs run
-                    auto tload = [&](frag (&t)[NLS], int task) {
+                    for (int task = w; task < ntask; task += kWaves) {
+                        frag tc[NLS];
                         const T* tsb = tptr(task);
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-                    };
-                    frag tc[NLS], tn[NLS];
-                    if (PF && w < ntask && !(ablate & 2)) tload(tc, w);
-                    for (int task = w; task < ntask; task += kWaves) {
-                        if (ablate & 2) break;
-                        if (!PF) tload(tc, task);
-                        else if (task + kWaves < ntask) tload(tn, task + kWaves);
-                        f32x4 a0 = {}, a1 = {};
+                        for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ls += NP) {
-                            seg_mma<T, X3>(a0, tc + ls, q0 + ls);
-                            seg_mma<T, X3>(a1, tc + ls, q1 + ls);
-                        }
-                        store(a0, a1, task);
-                        if (PF) {
+                        for (int s = 0; s < kQS; ++s) {
+                            f32x4 a = {};
 #pragma unroll
-                            for (int ls = 0; ls < NLS; ++ls) tc[ls] = tn[ls];
+                            for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(a, tc + ls, qf[s] + ls);
+                            store(a, s, task);
                         }
                     }
                 } else {
                     for (int task = w; task < ntask; task += kWaves) {
                         const T* tsb = tptr(task);
-                        f32x4 a0 = {}, a1 = {};
-                        for (int ls = 0; ls < nls * NP; ls += NP) {
-                            frag t[NP], u0[NP], u1[NP];
+                        f32x4 a[kQS];
 #pragma unroll
-                            for (int p = 0; p < NP; ++p) {
-                                t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
-                                u0[p] = *reinterpret_cast<const frag*>(qsb + ((size_t)(ls + p) * 64 + lane) * SG::LE);
-                                u1[p] = *reinterpret_cast<const frag*>(qsb1 + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                        for (int s = 0; s < kQS; ++s) a[s] = f32x4{};
+                        for (int ls = 0; ls < nls * NP; ls += NP) {
+                            frag t[NP];
+#pragma unroll
+                            for (int p = 0; p < NP; ++p) t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
+#pragma unroll
+                            for (int s = 0; s < kQS; ++s) {
+                                frag u[NP];
+#pragma unroll
+                                for (int p = 0; p < NP; ++p)
+                                    u[p] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                                seg_mma<T, X3>(a[s], t, u);
                             }
-                            seg_mma<T, X3>(a0, t, u0);
-                            seg_mma<T, X3>(a1, t, u1);
                         }
-                        store(a0, a1, task);
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) store(a[s], s, task);
                     }
                 }
                 __syncthreads();
@@ -416,10 +435,11 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 const int ty = sys[L][q] + r / K, tx = sxs[L][q] + r % K;
                 float acc = 0.f;
                 if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
-                    const T* qs = q < kBX ? qsb : qsb1;
+                    const int qr = q / kBX, qc = q % kBX;
+                    const T* qs = qsb[qr * QSX + qc / 16];
                     const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
                     for (int c = 0; c < g.C; ++c)
-                        acc = fmaf(seg_elem<T, X3>(qs, q % kBX, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
+                        acc = fmaf(seg_elem<T, X3>(qs, qc % 16, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
                 }
                 S[q * kLd + r] = acc;
             }
@@ -446,10 +466,6 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y >= g.H || x >= g.W) continue;
             const float fy = sfy[L][q] + (sfx[L][q] - sfx[L][q]);   // a NaN x weight reaches rows outside the band too
-            if (ablate & 1) {
-                if (hx[i][0] == 123.f) ob[0] = fy;       // keep the sums live
-                continue;
-            }
             float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
             for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
@@ -858,69 +874,61 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: radius %d not in 1..8", radius);
     hipStream_t st = as_stream(stream);
     const OtfGeom g = make_otf_geom(batch, channels, height, width, levels);
-    const long long nblk = (long long)((width + kBX - 1) / kBX) * ((height + kBY - 1) / kBY) * batch;
-    RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");
-    const size_t lds = sizeof(float) * kQ * kLd;
     const size_t qn = otf_query_elems(g);
     // compiled channel counts keep the query segments in registers; f32 operands of >= 128 channels
-    // would not fit and take the runtime loop (RMD_OTF_RUNTIME=1 forces it in the diagnostic build)
-    // RMD_OTF_ABLATE (diagnostic build only, results invalid): bits 1 = skip output stores, 2 = skip the MFMA
-    // phase
-    const int ablate = env_knob("RMD_OTF_ABLATE", 0);           // always 0 outside librmd_diag.so
-    const bool force_rt = env_knob("RMD_OTF_RUNTIME", 0) != 0;
-#ifdef RMD_DIAG
-    const bool pf = env_knob("RMD_OTF_PF", 0) != 0;
-#define RMD_OTF_K(T, RR, CC) (pf ? otf_lookup_kernel<T, XS, RR, CC, true> : otf_lookup_kernel<T, XS, RR, CC, false>)
-#else
-#define RMD_OTF_K(T, RR, CC) otf_lookup_kernel<T, XS, RR, CC, false>
-#endif
+    // would not fit and take the runtime loop
     const bool exact = compute == RMD_F32;
     const bool x3 = compute == RMD_BF16X3;
-    const int cpt = force_rt || (exact && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
-#define RMD_OTF(T, RR, CC)                                                                                     \
+    const int cpt = (exact && g.Cp >= 128) || g.Cp > 256 ? 0 : g.Cp;
+    // query block per compute: bf16 QSX_B x QSY_B segments, split-bf16 / f32 QSX_X x QSY_X (query
+    // fragments in registers: 8 (bf16) / 16 (x3) load steps per segment at C = 256)
+#define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
-        auto k = RMD_OTF_K(T, RR, CC);                                                                         \
+        using QB = QBlock<QX, QY>;                                                                             \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC>;                                                     \
+        const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
+        RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
+        const size_t lds = sizeof(float) * QB::kQ * kLd;                                                       \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
-        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn * XN, g, coords, zero_level_mask, out, ablate);   \
+        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn * XN, g, coords, zero_level_mask, out);          \
     } while (0)
-#define RMD_OTF_C(T, RR)                                 \
-    switch (cpt) {                                       \
-        case 32: RMD_OTF(T, RR, 32); break;              \
-        case 64: RMD_OTF(T, RR, 64); break;              \
-        case 128: RMD_OTF(T, RR, 128); break;            \
-        case 256: RMD_OTF(T, RR, 256); break;            \
-        default: RMD_OTF(T, RR, 0); break;               \
+#define RMD_OTF_C(T, RR, QX, QY, OC)                                 \
+    switch (cpt) {                                                   \
+        case 32: RMD_OTF(T, RR, 32, QX, QY, OC); break;              \
+        case 64: RMD_OTF(T, RR, 64, QX, QY, OC); break;              \
+        case 128: RMD_OTF(T, RR, 128, QX, QY, OC); break;            \
+        case 256: RMD_OTF(T, RR, 256, QX, QY, OC); break;            \
+        default: RMD_OTF(T, RR, 0, QX, QY, OC); break;               \
     }
-#define RMD_OTF_R(T)                                     \
-    switch (radius) {                                    \
-        case 1: RMD_OTF_C(T, 1); break;                  \
-        case 2: RMD_OTF_C(T, 2); break;                  \
-        case 3: RMD_OTF_C(T, 3); break;                  \
-        case 4: RMD_OTF_C(T, 4); break;                  \
-        case 5: RMD_OTF_C(T, 5); break;                  \
-        case 6: RMD_OTF_C(T, 6); break;                  \
-        case 7: RMD_OTF_C(T, 7); break;                  \
-        default: RMD_OTF_C(T, 8); break;                 \
+#define RMD_OTF_R(T, QX, QY, OC)                                     \
+    switch (radius) {                                                \
+        case 1: RMD_OTF_C(T, 1, QX, QY, OC); break;                  \
+        case 2: RMD_OTF_C(T, 2, QX, QY, OC); break;                  \
+        case 3: RMD_OTF_C(T, 3, QX, QY, OC); break;                  \
+        case 4: RMD_OTF_C(T, 4, QX, QY, OC); break;                  \
+        case 5: RMD_OTF_C(T, 5, QX, QY, OC); break;                  \
+        case 6: RMD_OTF_C(T, 6, QX, QY, OC); break;                  \
+        case 7: RMD_OTF_C(T, 7, QX, QY, OC); break;                  \
+        default: RMD_OTF_C(T, 8, QX, QY, OC); break;                 \
     }
     if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
-        RMD_OTF_R(__bf16)
+        RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
-        RMD_OTF_R(__bf16)
+        RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
-        RMD_OTF_R(float)
+        RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
 #undef RMD_OTF_R
 #undef RMD_OTF_C
 #undef RMD_OTF
-#undef RMD_OTF_K
     return check_launch("rmd_corr_otf_lookup");
 }
 

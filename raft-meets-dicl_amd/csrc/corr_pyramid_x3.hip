@@ -468,7 +468,7 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     // product: Q = 1.  Measured at cfg2 (profiles/x3_ab_r02_persist.json), bitwise identical:
     // Q = 1 0.632 ms, Q <= 2 0.619, Q = 4 (7 even slots) 0.627 — like the w8 GEMM, the kernel is
     // bound chip-wide (2.09 GB fp32 pyramid stream + the MFMA phases' overlap), not by CU balance
-    const int qmax = env_knob("RMD_X3_QMAX", 1);
+    constexpr int qmax = 1;
     for (int q = 1; q <= qmax && q * 8 <= nqt; q *= 2) {
         const long long units = (long long)nblk * d.batch * q;
         const int tq = (nqt + q - 1) / q;
@@ -483,15 +483,8 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const long long units = (long long)nblk * d.batch * quarters;
     const int nwg = (int)(units < ncu ? units : (quarters == 1 ? units : ncu));
     const int lds = kBlockRows * kBlockCols * kRow;
-    // product: ping-pong phases; the diagnostic build's RMD_X3_PP=0 runs free-running waves (A/B)
-#ifdef RMD_DIAG
-    auto kern = env_knob("RMD_X3_PP", 1) ? corr_pyramid_x3<true> : corr_pyramid_x3<false>;
-    if (env_knob("RMD_X3_PAD", 1) == 0) kern = corr_pyramid_x3<true, 0, false>;
-    if (env_knob("RMD_ABLATE", 0) == 1) kern = corr_pyramid_x3<true, 1>;
-    if (env_knob("RMD_ABLATE", 0) == 2) kern = corr_pyramid_x3<true, 2>;
-#else
+    // ping-pong phases (free-running waves measured slower, profiles/x3_ab_r02.json)
     auto kern = corr_pyramid_x3<true>;
-#endif
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nwg, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), (int)units, quarters, tq, reinterpret_cast<float*>(pyr));
     return check_launch("rmd_corr_pyramid/gemm-x3");

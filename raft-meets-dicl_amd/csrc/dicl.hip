@@ -396,7 +396,7 @@ dicl_stack_patch_kernel(const float* __restrict__ f1, const float* __restrict__ 
 constexpr int kWinFloats = 12288;      // 48 KiB LDS window
 constexpr int kWinSmall = 4096;        // 16 KiB LDS window (narrow maps, see rmd_dicl_stack_backward)
 
-template <int R, int WIN, int ABL = 0>
+template <int R, int WIN>
 __global__ void __launch_bounds__(kThreads)
 dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
                                  float* __restrict__ gf1, float* __restrict__ gf2) {
@@ -444,12 +444,8 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
                     const float* gd = gp + (size_t)(a * D + j) * dstride;
-                    if constexpr (ABL == 3) {
-                        gr[a] = fx * (float)(a + j);
-                    } else {
-                        s1 += gd[(size_t)c * n];
-                        gr[a] = gd[(size_t)(C + c) * n];
-                    }
+                    s1 += gd[(size_t)c * n];
+                    gr[a] = gd[(size_t)(C + c) * n];
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i)
@@ -467,10 +463,7 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
 #pragma unroll
                     for (int i = 0; i < K; ++i) {
                         const int xx = xs + i;
-                        if (ABL == 4) {      // diagnostic: same adds, consecutive ones on disjoint rows
-                            if (xx >= 0 && xx < P.wl) atomicAdd(win + ((j + i) % 24) * P.wl + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
-                        } else if (ABL != 2 && xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
-                        if (ABL == 2) s1 += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                        if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, qcur[i] * (1.0f - fy) + qprev[i] * fy);
                     }
                 } else {
                     float* r = g2c + (size_t)yy * P.wl;
@@ -490,197 +483,15 @@ dicl_stack_patch_backward_kernel(const float* __restrict__ g, const float* __res
     float* gw = g2c + (size_t)wy0 * P.wl;
     for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
         const float v = win[k];
-        if (ABL != 1 && v != 0.f) atomicAdd(gw + k, v);
-    }
-}
-
-// Same backward with 4 consecutive pixels per lane.  LDS float atomics are the cost of the one-pixel
-// kernel (0.98 ms at cfg4, 0.23 ms with them dropped: ~100 cycles per ds_add_f32 wave-instruction),
-// so a lane first merges its pixels' patch rows in registers: when the 4 patches share a top row
-// and start at consecutive columns (smooth flow: the common case) row j of the 4 patches is one
-// (2r+5)-wide run, 13 adds instead of 40 at r = 4.  Otherwise every pixel adds its own row.  The
-// gradient rows are read as float4 (1 KiB per wave-instruction).  grid (pixels/1024, C, B).
-template <int R, int WIN, int PX, bool CHAIN>
-__global__ void __launch_bounds__(kThreads)
-dicl_stack_patch_backward4_kernel(const float* __restrict__ g, const float* __restrict__ coords, StackParams P,
-                                  float* __restrict__ gf1, float* __restrict__ gf2) {
-    constexpr int D = 2 * R + 1, K = 2 * R + 2, M = K + PX - 1;
-    __shared__ float win[WIN];
-    __shared__ int wmin;
-    const int n = P.h * P.w, nl = P.hl * P.wl;
-    const int p0 = (blockIdx.x * kThreads + threadIdx.x) * PX;
-    const int c = blockIdx.y, b = blockIdx.z;
-    const bool pv = p0 < n;               // n % 4 == 0: a lane's PX pixels are all valid or all not
-    float fx[PX], fy[PX];
-    int xs[PX], ys[PX];
-    int ymin = 1 << 30;
-#pragma unroll
-    for (int k = 0; k < PX; ++k) {
-        fx[k] = fy[k] = 0.f;
-        xs[k] = 0;
-        ys[k] = 1 << 30;
-        if (pv) {
-            float cx = coords[(size_t)b * 2 * n + p0 + k] * P.inv_scale;
-            float cy = coords[(size_t)b * 2 * n + n + p0 + k] * P.inv_scale;
-            cx = fminf(fmaxf(cx, -1.0e6f), 1.0e6f);
-            cy = fminf(fmaxf(cy, -1.0e6f), 1.0e6f);
-            const float fx0 = floorf(cx), fy0 = floorf(cy);
-            fx[k] = cx - fx0;
-            fy[k] = cy - fy0;
-            xs[k] = (int)fx0 - R;
-            ys[k] = (int)fy0 - R;
-            ymin = min(ymin, max(ys[k], 0));
-        }
-    }
-    bool merged = true;
-#pragma unroll
-    for (int k = 1; k < PX; ++k) merged = merged && ys[k] == ys[0] && xs[k] == xs[0] + k;
-    merged = merged && pv;
-    // CHAIN: lane l's merged run continues lane l-1's (same patch top row, start PX columns further)
-    // -> the wave sums overlapping runs with DPP lane shifts and each lane adds only its own PX
-    // columns (a chain's last lane adds its whole tail): 2 LDS adds per row instead of 2r+2+PX-1.
-    bool link = false, link_next = false;
-    if constexpr (CHAIN) {
-        const int pys = __builtin_amdgcn_update_dpp((int)0x80000000, ys[0], 0x138, 0xf, 0xf, false);   // wave_shr:1
-        const int pxs = __builtin_amdgcn_update_dpp((int)0x80000000, xs[0], 0x138, 0xf, 0xf, false);
-        const int pm = __builtin_amdgcn_update_dpp(0, (int)merged, 0x138, 0xf, 0xf, false);
-        link = merged && pm != 0 && pys == ys[0] && pxs + PX == xs[0];
-        link_next = __builtin_amdgcn_update_dpp(0, (int)link, 0x130, 0xf, 0xf, false) != 0;              // wave_shl:1
-    }
-    if (threadIdx.x == 0) wmin = 1 << 30;
-    for (int k = threadIdx.x; k < WIN; k += kThreads) win[k] = 0.f;
-    __syncthreads();
-    if (pv) atomicMin(&wmin, ymin);
-    __syncthreads();
-    const int wy0 = min(wmin, P.hl);
-    const int wrows = min(P.hl - wy0, WIN / P.wl);
-    const int C = P.C, C2 = 2 * C + P.extra;
-    const size_t dstride = (size_t)C2 * n;
-    float* g2c = gf2 + ((size_t)b * C + c) * nl;
-    typedef typename FVec<PX>::T v4;
-    if (pv) {
-        // wave-uniform plane base + 32-bit lane offsets (saddr + voffset; the host keeps a batch
-        // image's gradient volume below 4 GiB)
-        const char* gb = reinterpret_cast<const char*>(g + (size_t)b * D * D * dstride);
-        const unsigned lo1 = (unsigned)(((size_t)c * n + p0) * sizeof(float));
-        const unsigned lo2 = lo1 + (unsigned)((size_t)C * n * sizeof(float));
-        v4 s1 = v4(0.f);
-        float qprev[PX][K];
-#pragma unroll
-        for (int k = 0; k < PX; ++k)
-#pragma unroll
-            for (int i = 0; i < K; ++i) qprev[k][i] = 0.f;
-#pragma unroll 1
-        for (int j = 0; j < K; ++j) {      // rolled: unrolled, the scheduler hoists later rows' loads (256 VGPRs)
-            float qcur[PX][K];
-            if (j < D) {
-                v4 gr[D];
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    const char* gd = gb + (size_t)(a * D + j) * dstride * sizeof(float);
-                    s1 += *reinterpret_cast<const v4*>(gd + lo1);
-                    gr[a] = *reinterpret_cast<const v4*>(gd + lo2);
-                }
-#pragma unroll
-                for (int k = 0; k < PX; ++k)
-#pragma unroll
-                    for (int i = 0; i < K; ++i)
-                        qcur[k][i] = (i < D ? gr[i][k] * (1.0f - fx[k]) : 0.f) + (i >= 1 ? gr[i - 1][k] * fx[k] : 0.f);
-            } else {
-#pragma unroll
-                for (int k = 0; k < PX; ++k)
-#pragma unroll
-                    for (int i = 0; i < K; ++i) qcur[k][i] = 0.f;
-            }
-            // row j of the patches, computed in place of the previous row's x-spread
-            float (&val)[PX][K] = qprev;
-#pragma unroll
-            for (int k = 0; k < PX; ++k)
-#pragma unroll
-                for (int i = 0; i < K; ++i) val[k][i] = qcur[k][i] * (1.0f - fy[k]) + qprev[k][i] * fy[k];
-            if (merged) {
-                const int yy = ys[0] + j;
-                if (yy >= 0 && yy < P.hl) {
-                    float m[M];
-#pragma unroll
-                    for (int t = 0; t < M; ++t) {
-                        float acc = 0.f;
-#pragma unroll
-                        for (int k = 0; k < PX; ++k)
-                            if (t - k >= 0 && t - k < K) acc += val[k][t - k];
-                        m[t] = acc;
-                    }
-                    if constexpr (CHAIN) {
-                        // r_t = sum over the chain's lanes l-k of m_{l-k}[t + PX k]: all at column xs_l + t
-#pragma unroll
-                        for (int t = 0; t < M; ++t) {
-                            const int kmax = (M - 1 - t) / PX;
-                            float rr = m[t + PX * kmax];
-#pragma unroll
-                            for (int k = kmax - 1; k >= 0; --k) {
-                                const float up = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rr), 0x138, 0xf, 0xf, false));
-                                rr = m[t + PX * k] + (link ? up : 0.f);
-                            }
-                            m[t] = (t < PX || !link_next) ? rr : 0.f;
-                        }
-                    }
-                    if (yy - wy0 < wrows) {      // LDS / global in separate branches (no flat atomics)
-                        float* r = win + (yy - wy0) * P.wl;
-#pragma unroll
-                        for (int t = 0; t < M; ++t) {
-                            const int xx = xs[0] + t;
-                            if (xx >= 0 && xx < P.wl && (!CHAIN || t < PX || !link_next)) atomicAdd(r + xx, m[t]);
-                        }
-                    } else {
-                        float* r = g2c + (size_t)yy * P.wl;
-#pragma unroll
-                        for (int t = 0; t < M; ++t) {
-                            const int xx = xs[0] + t;
-                            if (xx >= 0 && xx < P.wl && (!CHAIN || t < PX || !link_next)) atomicAdd(r + xx, m[t]);
-                        }
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < PX; ++k) {
-                    const int yy = ys[k] + j;
-                    if (yy < 0 || yy >= P.hl) continue;
-                    if (yy - wy0 < wrows) {
-                        float* r = win + (yy - wy0) * P.wl;
-#pragma unroll
-                        for (int i = 0; i < K; ++i) {
-                            const int xx = xs[k] + i;
-                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, val[k][i]);
-                        }
-                    } else {
-                        float* r = g2c + (size_t)yy * P.wl;
-#pragma unroll
-                        for (int i = 0; i < K; ++i) {
-                            const int xx = xs[k] + i;
-                            if (xx >= 0 && xx < P.wl) atomicAdd(r + xx, val[k][i]);
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < PX; ++k)
-#pragma unroll
-                for (int i = 0; i < K; ++i) qprev[k][i] = qcur[k][i];
-        }
-        *reinterpret_cast<v4*>(gf1 + ((size_t)b * C + c) * n + p0) = s1;
-    }
-    __syncthreads();
-    float* gw = g2c + (size_t)wy0 * P.wl;
-    for (int k = threadIdx.x; k < wrows * P.wl; k += kThreads) {
-        const float v = win[k];
         if (v != 0.f) atomicAdd(gw + k, v);
     }
 }
 
+
 // Same backward, 2 pixels per lane, with a GENERAL merge of the lane's two patches: whenever the
 // pixels' integer window origins differ by at most 1 row and 2 columns (any smooth flow), the two
 // (2r+2)^2 patches are summed in registers over their joint box of (2r+3) rows x (2r+4) columns and
-// every lane adds one run of 2r+4 values per joint row.  backward4 merges only origins exactly one
+// every lane adds one run of 2r+4 values per joint row.  The round-1 kernel merged only origins exactly one
 // column apart and sends every other lane through a per-pixel path of 2 (2r+2) adds per row; because
 // a wave executes every path one of its lanes takes, a wave with both kinds paid for both (the
 // cost of the LDS atomics, ~100 cycles per ds_add_f32 wave-instruction, is per instruction).  Here
@@ -1249,47 +1060,7 @@ dicl_nz_kernel(const float* __restrict__ f2, IntParams P, unsigned char* __restr
     nz[(size_t)b * n + p] = s != 0.f;
 }
 
-// grid: (pixels/4 per row chunk, du*dv, B); lane = 4 consecutive pixels of one displacement plane
-__global__ void __launch_bounds__(kThreads)
-dicl_stack_int_kernel(const float* __restrict__ f1, const float* __restrict__ f2,
-                      const unsigned char* __restrict__ nz, IntParams P, float* __restrict__ out) {
-    const int n = P.h * P.w;
-    const int quad = blockIdx.x * kThreads + threadIdx.x;
-    const int p0 = quad * 4;
-    if (p0 >= n) return;
-    const int dv = 2 * P.rv + 1;
-    const int disp = blockIdx.y;                 // i * dv + j
-    const int i = disp / dv, jj = disp - i * dv;
-    const int di = i - P.ru, dj = jj - P.rv;
-    const int b = blockIdx.z;
-    const int C = P.C;
-    int src[4];
-    bool ok[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int p = p0 + k;
-        const int y = p / P.w, x = p - y * P.w;
-        const int xx = x + di, yy = y + dj;
-        const bool inb = xx >= 0 && xx < P.w && yy >= 0 && yy < P.h;
-        src[k] = inb ? yy * P.w + xx : 0;
-        ok[k] = inb && nz[(size_t)b * n + src[k]];
-    }
-    const int du_dv = (2 * P.ru + 1) * dv;
-    float* o = out + ((size_t)(b * du_dv + disp) * 2 * C) * n + p0;
-    const float* f1b = f1 + (size_t)b * C * n + p0;
-    const float* f2b = f2 + (size_t)b * C * n;
-    for (int c = 0; c < C; ++c) {
-        const float4 a = *reinterpret_cast<const float4*>(f1b + (size_t)c * n);
-        const float* f2c = f2b + (size_t)c * n;
-        *reinterpret_cast<float4*>(o + (size_t)c * n) =
-            make_float4(ok[0] ? a.x : 0.f, ok[1] ? a.y : 0.f, ok[2] ? a.z : 0.f, ok[3] ? a.w : 0.f);
-        *reinterpret_cast<float4*>(o + (size_t)(C + c) * n) =
-            make_float4(ok[0] ? f2c[src[0]] : 0.f, ok[1] ? f2c[src[1]] : 0.f, ok[2] ? f2c[src[2]] : 0.f,
-                        ok[3] ? f2c[src[3]] : 0.f);
-    }
-}
-
-// Same output as dicl_stack_int_kernel, restructured for the write stream: a 1-D grid remapped per
+// Integer volume (impls/dicl.py:212-238), written for the write stream: a 1-D grid remapped per
 // XCD (one batch image's f1/f2 — 2 x 1.5 MB at cfg3 level 2 — stay in that XCD's L2 while its 49
 // displacement planes re-read them), the channel loop unrolled by U so a lane's loads of U channels
 // are all in flight before its 2U stores, and optionally non-temporal stores (the 1.2 GB volume is
@@ -1347,27 +1118,19 @@ dicl_stack_int_v2_kernel(const float* __restrict__ f1, const float* __restrict__
     }
 }
 
-// launch the integer volume (nz already computed); RMD_DICL_INT selects a variant for A/B runs
-// (tools/dicl_ab.py): 1 = the first kernel, 2 = plain stores, 3 = XCD remap, 4 = 8 waves per SIMD forced.  Measured at cfg3
-// (profiles/dicl_ab_r01.json): 0.366 ms (first) -> 0.234 ms (default: unrolled, nt, no remap)
+// launch the integer volume (nz already computed).  Measured at cfg3 (profiles/dicl_ab_r01.json): 0.366 ms
+// for the first formulation (3-D grid, rolled channel loop) -> 0.234 ms (unrolled, non-temporal stores,
+// no XCD remap); 8 waves per SIMD forced is slower (0.235 ms, profiles/dicl_int_wpe_ab_r02.json)
 int launch_stack_int(const float* fmap1, const float* fmap2, const unsigned char* nz, const IntParams& P,
                      float* out, hipStream_t st) {
     const int n = P.h * P.w;
     const int ndisp = (2 * P.ru + 1) * (2 * P.rv + 1);
-    const int var = env_variant("RMD_DICL_INT");
-    if (var == 1) {          // the first formulation (3-D grid, rolled channel loop)
-        dim3 grid((n / 4 + kThreads - 1) / kThreads, ndisp, P.B);
-        dicl_stack_int_kernel<<<grid, kThreads, 0, st>>>(fmap1, fmap2, nz, P, out);
-        return check_launch("rmd_dicl_stack_int");
-    }
     const int nqb = (n / 4 + kThreads - 1) / kThreads;
     const long long nwg = (long long)nqb * ndisp * P.B;
     RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack_int: grid too large");
-    const bool nt = var != 2, remap = var == 3;
+    const bool remap = false;
     if (P.C == 32) {
-        if (var == 4) dicl_stack_int_v2_kernel<32, true, 8><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
-        else if (nt) dicl_stack_int_v2_kernel<32, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
-        else dicl_stack_int_v2_kernel<32, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
+        dicl_stack_int_v2_kernel<32, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
     } else {
         dicl_stack_int_v2_kernel<0, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, nz, P, nqb, remap, out);
     }
@@ -1625,171 +1388,6 @@ dap_x3_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D,
     }
 }
 
-#ifdef RMD_DIAG
-// MFMA form (exact f32: v_mfma_f32_32x32x2_f32 == an fmaf chain): a workgroup owns 32 output
-// displacements x 128 pixels (4 waves x 32 pixels); its 32 rows of W (or of W^T) sit in LDS with an
-// odd row stride, x is read as two 128-B row segments per k-step.  grid (pixels/128, D/32, B).
-
-__global__ void __launch_bounds__(kThreads)
-dap_mfma_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
-                float* __restrict__ out) {
-    extern __shared__ float sw[];                       // 32 rows x (Dk + 1), Dk = D rounded up to even
-    const int Dk = (D + 1) & ~1, ld = Dk + 1;
-    const int o0 = blockIdx.y * 32, b = blockIdx.z;
-    for (int k = threadIdx.x; k < 32 * Dk; k += kThreads) {
-        const int r = k / Dk, i = k - r * Dk, o = o0 + r;
-        float v = 0.f;
-        if (o < D && i < D) v = transpose ? wgt[(size_t)i * D + o] : wgt[(size_t)o * D + i];
-        sw[r * ld + i] = v;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int j = lane & 31, h = lane >> 5;
-    const int p = blockIdx.x * 128 + w * 32 + j;
-    const bool pv = p < n;
-    const float* xb = x + (size_t)b * D * n + (pv ? p : 0);
-    f32x16_t acc = {};
-    int k = 0;
-    for (; k + 16 <= Dk; k += 16) {
-        float av[8], bv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int kk = k + 2 * u + h;
-            av[u] = sw[j * ld + kk];
-            bv[u] = (kk < D && pv) ? xb[(size_t)kk * n] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
-    }
-    for (; k < Dk; k += 2) {
-        const int kk = k + h;
-        const float bv = (kk < D && pv) ? xb[(size_t)kk * n] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[j * ld + kk], bv, acc, 0, 0, 0);
-    }
-    if (!pv) return;
-    float* ob = out + (size_t)b * D * n + p;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const int o = o0 + 8 * (e >> 2) + 4 * h + (e & 3);
-        if (o < D) ob[(size_t)o * n] = acc[e];
-    }
-}
-
-#ifndef RMD_DAP_KC
-#define RMD_DAP_KC 8
-#endif
-// Blocked MFMA form: a workgroup (4 waves) owns an M-block of MT x 32 output displacements — all D
-// of them when D <= 128 — whose rows of W (or W^T) sit in LDS once, and its waves loop over 32-pixel
-// tiles; each x value is read from HBM once per M-block (once in all for D <= 128) and feeds MT
-// MFMAs.  The kernel is latency-bound, not bandwidth- or MFMA-bound (one round of ~2 waves per SIMD at
-// cfg4), so with KS > 0 (D <= 2 KS) a wave issues ALL of its tile's x loads (KS k-steps of 2 rows)
-// before the workgroup stages W and before any MFMA: one memory round trip per tile instead of one
-// per 8-row batch.  KS = 0 streams x in chunks of RMD_DAP_KC k-steps, two chunks in flight (large D).
-// x loads and out stores are buffer instructions on the batch slab (lane offset + scalar row
-// offset; rows >= D and pixels >= n fall outside the range: loads read 0, stores are dropped).
-// grid (workgroups per (M-block, batch), M-blocks, B).
-// Diagnostic build only (RMD_DAP_VALU=3): kernel time equals the round-1 form's at D = 81 (22.5 vs
-// 23.4 us), is slower at D = 49 (20.5 vs 17.2) and faster only for D = 324 with 4 tiles per wave
-// (240 vs 308 us) — profiles/dap_ab_r02.json.  The exact-f32 MFMA chain (64 cycles per
-// v_mfma_f32_32x32x2_f32) at ~2 waves per SIMD bounds every variant near 25 % of the f32 MFMA peak.
-template <int MT, int KS>
-__global__ void __launch_bounds__(kThreads)
-dap_mfma_blk_kernel(const float* __restrict__ x, const float* __restrict__ wgt, int D, int n, int transpose,
-                    float* __restrict__ out) {
-    extern __shared__ float sw[];                       // MT*32 rows x (Dk + 1)
-    const int Dk = (D + 1) & ~1, ld = Dk + 1;
-    const int o0 = blockIdx.y * 32 * MT, b = blockIdx.z;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int j = lane & 31, h = lane >> 5;
-    const int ntile = (n + 31) >> 5;
-    const float* xb0 = x + (size_t)b * D * n;
-    float* ob0 = out + (size_t)b * D * n;
-    auto rsrc = [&](const void* base) {
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
-        return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
-                                                 (int)((unsigned)D * (unsigned)n * 4u), 0x00020000);
-    };
-    const __amdgpu_buffer_rsrc_t xr = rsrc(xb0);
-    const __amdgpu_buffer_rsrc_t orr = rsrc(ob0);
-    const unsigned rowb = (unsigned)n * 4u;              // bytes per displacement row
-    auto xoff = [&](int t, int k0) {                     // lane offset of rows 2 k0 + h, pixel of tile t
-        const int p = t * 32 + j;
-        return p < n ? (int)((unsigned)(2 * k0 + h) * rowb + (unsigned)p * 4u) : (int)0x80000000;
-    };
-    int t = blockIdx.x * 4 + w;
-    float xv[KS > 0 ? KS : 1];
-    if constexpr (KS > 0) {
-        const int vo = xoff(t < ntile ? t : 0, 0);
-#pragma unroll
-        for (int u = 0; u < KS; ++u)
-            xv[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
-    }
-    for (int k = threadIdx.x; k < 32 * MT * Dk; k += kThreads) {
-        const int r = k / Dk, i = k - r * Dk, o = o0 + r;
-        float v = 0.f;
-        if (o < D && i < D) v = transpose ? wgt[(size_t)i * D + o] : wgt[(size_t)o * D + i];
-        sw[r * ld + i] = v;
-    }
-    __syncthreads();
-    const int nks = Dk >> 1;                               // k-steps of 2 rows
-    for (bool first = true; t < ntile; t += gridDim.x * 4, first = false) {
-        f32x16_t acc[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] = f32x16_t{};
-        if constexpr (KS > 0) {
-            if (!first) {
-                const int vo = xoff(t, 0);
-#pragma unroll
-                for (int u = 0; u < KS; ++u)
-                    xv[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
-            }
-#pragma unroll
-            for (int u = 0; u < KS; ++u) {
-                if (u < nks) {
-                    const int kk = 2 * u + h;
-#pragma unroll
-                    for (int m = 0; m < MT; ++m)
-                        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[(m * 32 + j) * ld + kk], xv[u], acc[m], 0, 0, 0);
-                }
-            }
-        } else {
-            constexpr int KC = RMD_DAP_KC;
-            float cur[KC], nxt[KC];
-            auto load_chunk = [&](float (&v)[KC], int c0) {
-                const int vo = xoff(t, c0);
-#pragma unroll
-                for (int u = 0; u < KC; ++u)
-                    v[u] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, (int)((unsigned)u * 2u * rowb), 0));
-            };
-            load_chunk(cur, 0);
-            for (int c0 = 0; c0 < nks; c0 += KC) {
-                if (c0 + KC < nks) load_chunk(nxt, c0 + KC);
-#pragma unroll
-                for (int u = 0; u < KC; ++u) {
-                    if (c0 + u < nks) {
-                        const int kk = 2 * (c0 + u) + h;
-#pragma unroll
-                        for (int m = 0; m < MT; ++m)
-                            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(sw[(m * 32 + j) * ld + kk], cur[u], acc[m], 0, 0, 0);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < KC; ++u) cur[u] = nxt[u];
-            }
-        }
-        // C tile: lane (j, h) holds rows 8 (e >> 2) + 4 h + (e & 3) of pixel column j
-        const int p = t * 32 + j;
-        const int so = p < n ? (int)((unsigned)(4 * h) * rowb + (unsigned)p * 4u) : (int)0x80000000;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int e = 0; e < 16; ++e)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[m][e]), orr, so,
-                                                      (int)((unsigned)(o0 + m * 32 + 8 * (e >> 2) + (e & 3)) * rowb), 0);
-    }
-}
-#endif  // RMD_DIAG
 
 int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int radius, int level, int nh, int nw,
                  int extra) {
@@ -1810,7 +1408,7 @@ int stack_params(StackParams& P, int B, int C, int h, int w, int hl, int wl, int
 // warped[c, p] = mask(p) * bilinear(img2[c], x + fx, y + fy) with zero padding, where mask(p) = the
 // in-bounds bilinear weight > 1 - eps (grid_sample of a ones tensor, warp.py:28-30).  One lane per pixel
 // loops over the channels; with NZ it also writes the occlusion flag sum_c warped[c, p] != 0 that
-// dicl_stack_int_kernel consumes, so the warp costs no extra pass over the warped map.
+// integer-volume kernel consumes, so the warp costs no extra pass over the warped map.
 struct WarpTaps {
     int idx[4];
     float wgt[4];
@@ -1904,24 +1502,18 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
     const int d = 2 * radius + 1;
     const double image_bytes = 4.0 * d * d * (2.0 * channels + P.extra) * height * width;
     if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4 && image_bytes < 4294967296.0) {
-        // RMD_DICL_PATCH (A/B, tools/dicl_ab.py): 1 = plain stores (2 pixels per lane), 2 = XCD remap
-        // (2 pixels), 3 = 4 pixels per lane, 4 = 2 pixels per lane (round-1 product), 5 = 1 pixel + XCD remap.
         // Measured at cfg4 (profiles/dicl_ab_r01.json, dicl_px_ab_r02.json): non-temporal stores are the
-        // win (0.33 -> 0.26 ms); one pixel per lane (56 VGPRs, 7 waves per SIMD instead of 4) keeps more
-        // stores in flight: 0.238 vs 0.256 ms
-        const int var = env_variant("RMD_DICL_PATCH");
-        const int px = var == 3 ? 4 : (var == 0 || var == 5) ? 1 : 2;
+        // win (0.33 -> 0.26 ms); one pixel per lane (56 VGPRs, 7 waves per SIMD instead of 4 with 2 or 4
+        // pixels per lane) keeps more stores in flight: 0.238 vs 0.256 ms; an XCD remap changes nothing
+        constexpr int px = 1;
         const int nxb = (height * width / px + kThreads - 1) / kThreads;
         const long long nwg = (long long)nxb * channels * batch;
         RMD_REQUIRE(nwg < (1ll << 31), RMD_ERR_SHAPE, "rmd_dicl_stack: grid too large");
-        const int remap = var == 2 || var == 5;
+        constexpr int remap = 0;
         hipStream_t st = as_stream(stream);
         switch (radius) {
 #define RMD_CASE(RR) case RR: \
-            if (var == 1) dicl_stack_patch_kernel<RR, 2, false><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
-            else if (var == 3) dicl_stack_patch_kernel<RR, 4, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
-            else if (var == 2 || var == 4) dicl_stack_patch_kernel<RR, 2, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
-            else dicl_stack_patch_kernel<RR, 1, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
+            dicl_stack_patch_kernel<RR, px, true><<<(unsigned)nwg, kThreads, 0, st>>>(fmap1, fmap2, coords, P, nxb, remap, out); \
             break;
             RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE
@@ -1929,10 +1521,7 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
         return check_launch("rmd_dicl_stack/patch");
     }
     dim3 grid((height * width / 4 + kThreads - 1) / kThreads, d * d, batch);
-    // RMD_DICL_GENERAL (A/B, tools/dicl_ab.py): 1 = plain stores, 2 = channel loop unrolled by 2,
-    // 3 = per-tap kernel instead of the separable one
-    const int var = env_variant("RMD_DICL_GENERAL");
-    if (var == 0 && (radius == 3 || radius == 4) && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sx >= 0.f &&
+    if ((radius == 3 || radius == 4) && std::isfinite(P.sx) && std::isfinite(P.sy) && P.sx >= 0.f &&
         P.sy >= 0.f && P.sx <= 1.f && P.sy <= 1.f && image_bytes < 4294967296.0) {
         const float span = 2.0f * radius * std::max(P.sx, P.sy);
         const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
@@ -1947,12 +1536,7 @@ extern "C" int rmd_dicl_stack(const float* fmap1, const float* fmap2, const floa
         }
         if (launched) return check_launch("rmd_dicl_stack/separable");
     }
-    if (var == 1)
-        dicl_stack_kernel<false, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
-    else if (var == 2)
-        dicl_stack_kernel<true, 2><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
-    else
-        dicl_stack_kernel<true, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
+    dicl_stack_kernel<true, 1><<<grid, kThreads, 0, as_stream(stream)>>>(fmap1, fmap2, coords, P, out);
     return check_launch("rmd_dicl_stack");
 }
 
@@ -1970,54 +1554,30 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
     // LDS window: a workgroup's 256 pixels cover ~256/w + 1 rows; with the patch (<= 2r+2 rows at
     // unit steps) and some flow spread, 4096 floats (16 KiB) hold them for w up to ~170 and leave
     // room for 9 workgroups per CU instead of 3 (48 KiB); rows past the window still go to global
-    // atomics, so the choice only affects speed.  RMD_DICL_BWD_WIN=1 forces the 48 KiB window (A/B).
+    // atomics, so the choice only affects speed.
     const float rows_est = 2.0f * radius * std::max(P.sy, 1.0f) + 256.0f / width * std::max(P.sy, 0.5f) + 10.0f;
-    const bool small_win = rows_est * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
+    const bool small_win = rows_est * level_width <= (float)kWinSmall;
     const double image_bytes = 4.0 * d * d * (2.0 * channels + P.extra) * height * width;
     if (P.sx == 1.0f && P.sy == 1.0f && radius >= 1 && radius <= 4) {
         (void)hipMemsetAsync(grad_fmap2, 0, sizeof(float) * (size_t)batch * channels * level_height * level_width, st);
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
-        // 4 pixels per lane with merged patch rows (default), RMD_DICL_BWD_PX=1: one pixel per lane
-        if (env_variant("RMD_DICL_BWD_PX") != 1 && env_variant("RMD_DICL_BWD_ABL") == 0 && image_bytes < 4294967296.0) {
-            const int px = env_variant("RMD_DICL_BWD_PX") == 4 ? 4 : 2;     // 4: A/B (256 VGPRs at r = 4)
-            const float rows4 = 2.0f * radius + 256.0f * px / width + 10.0f;
-            const bool small4 = rows4 * level_width <= (float)kWinSmall && env_variant("RMD_DICL_BWD_WIN") != 1;
-            dim3 grid4((height * width / px + kThreads - 1) / kThreads, channels, batch);
-            const bool chain = env_variant("RMD_DICL_BWD_CHAIN") != 1;     // 1: no cross-lane run merge (A/B)
-            // product: general two-pixel merge + cross-lane chain (0.55 vs 0.75 ms smooth flow, 0.77 vs 0.96
-            // ms steep flow at cfg4, profiles/dicl_bwd_ab_r02.json); diagnostic RMD_DICL_BWD_GM: 2 selects
-            // backward4, 1 the merge without the chain
-            const bool gmerge = env_variant("RMD_DICL_BWD_GM") != 2 && env_variant("RMD_DICL_BWD_PX") != 4 &&
-                                env_variant("RMD_DICL_BWD_CHAIN") != 1 && env_variant("RMD_DICL_BWD_WIN") != 1;
-            const bool gchain = env_variant("RMD_DICL_BWD_GM") != 1;       // 1 (diagnostic): merge without the chain
+        // two pixels per lane: the general two-pixel merge over the joint patch box + the cross-lane chain
+        // (0.55 vs 0.75 ms smooth flow, 0.77 vs 0.96 ms steep flow at cfg4 against the round-1 per-pixel
+        // adds, profiles/dicl_bwd_ab_r02.json); one pixel per lane for images past 4 GiB of stack
+        if (image_bytes < 4294967296.0) {
+            const float rows2 = 2.0f * radius + 512.0f / width + 10.0f;
+            const bool small2 = rows2 * level_width <= (float)kWinSmall;
+            dim3 grid2((height * width / 2 + kThreads - 1) / kThreads, channels, batch);
             switch (radius) {
 #define RMD_CASE(RR) case RR: \
-                if (gmerge && gchain && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (gmerge && gchain) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (gmerge && small4) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (gmerge) dicl_stack_patch_backward_gm_kernel<RR, kWinFloats, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (px == 4 && small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (px == 4) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 4, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (small4 && chain) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (small4) dicl_stack_patch_backward4_kernel<RR, kWinSmall, 2, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else if (chain) dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2, true><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
-                else dicl_stack_patch_backward4_kernel<RR, kWinFloats, 2, false><<<grid4, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                if (small2) dicl_stack_patch_backward_gm_kernel<RR, kWinSmall, true><<<grid2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
+                else dicl_stack_patch_backward_gm_kernel<RR, kWinFloats, true><<<grid2, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
                 break;
                 RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4)
 #undef RMD_CASE
             }
-            return check_launch("rmd_dicl_stack_backward/patch4");
+            return check_launch("rmd_dicl_stack_backward/patch2");
         }
-#ifdef RMD_DIAG
-        const int abl = env_variant("RMD_DICL_BWD_ABL");     // diagnostic ablation (results wrong)
-        if (radius == 4 && abl >= 1 && abl <= 4 && P.wl * 24 <= kWinSmall) {
-            if (abl == 1) dicl_stack_patch_backward_kernel<4, kWinSmall, 1><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
-            if (abl == 2) dicl_stack_patch_backward_kernel<4, kWinSmall, 2><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
-            if (abl == 3) dicl_stack_patch_backward_kernel<4, kWinSmall, 3><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
-            if (abl == 4) dicl_stack_patch_backward_kernel<4, kWinSmall, 4><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2);
-            return check_launch("rmd_dicl_stack_backward/patch-ablation");
-        }
-#endif
         switch (radius) {
 #define RMD_CASE(RR) case RR: \
             if (small_win) dicl_stack_patch_backward_kernel<RR, kWinSmall><<<grid, kThreads, 0, st>>>(grad_stack, coords, P, grad_fmap1, grad_fmap2); \
@@ -2035,9 +1595,9 @@ extern "C" int rmd_dicl_stack_backward(const float* grad_stack, const float* coo
         const float span = 2.0f * radius * std::max(P.sx, P.sy);
         const int k = ((int)std::floor(span * (1.0f + 1e-5f) + 1e-4f) + 3 + 1) & ~1;
         dim3 grid((height * width + kThreads - 1) / kThreads, channels, batch);
-        // two pixels per lane with the merged / chained patch adds (K <= 8); RMD_DICL_BWD_SEP2=2
-        // (diagnostic) selects the one-pixel kernel
-        if (k <= 8 && env_variant("RMD_DICL_BWD_SEP2") != 2) {
+        // two pixels per lane with the merged / chained patch adds (K <= 8: 0.50 vs 0.68 ms smooth, 0.52 vs
+        // 0.61 ms steep flow at cfg4 level 1 against one pixel per lane); K > 8 one pixel per lane
+        if (k <= 8) {
             const float rows2 = 2.0f * radius * std::max(P.sy, 1.0f) + 512.0f / width * std::max(P.sy, 0.5f) + 10.0f;
             const bool small2 = rows2 * level_width <= (float)kWinSmall;
             dim3 grid2((height * width / 2 + kThreads - 1) / kThreads, channels, batch);
@@ -2249,80 +1809,23 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
                        float* out, void* stream) {
     RMD_REQUIRE(x && weight && out, RMD_ERR_ARG, "rmd_dap: null pointer");
     RMD_REQUIRE(batch > 0 && disp > 0 && pixels > 0, RMD_ERR_SHAPE, "rmd_dap: bad sizes");
-#ifdef RMD_DIAG
-    if (disp <= 1024 && (size_t)disp * pixels * 4 < (1ull << 31) && env_variant("RMD_DAP_VALU") == 3) {
-        // blocked kernel: M-blocks of up to 4 MFMA row tiles (128 displacements), W block in LDS
-        // (the M-block shrinks until its W rows fit in 150 KB of LDS: D = 81 -> one block of 3 tiles,
-        // D = 324 -> 4 blocks of 3)
-        const int Dk = (disp + 1) & ~1;
-        const int mt_all = (disp + 31) / 32;
-        int mt = mt_all < 4 ? mt_all : 4;
-        while (mt > 1 && (size_t)32 * mt * (Dk + 1) * sizeof(float) > 150 * 1024) --mt;
-        const int mblocks = (mt_all + mt - 1) / mt;
-        const size_t lds = sizeof(float) * 32 * mt * (size_t)(Dk + 1);
-        const int ntile = (pixels + 31) / 32;
-        // workgroups per (M-block, batch): TPW pixel tiles per wave (diagnostic knob RMD_DAP_TPW, product 1),
-        // capped at ~8 workgroups per CU chip-wide
-        const int tpw = env_knob("RMD_DAP_TPW", 1);
-        int per = (ntile + 4 * tpw - 1) / (4 * tpw);
-        const int cap = (2048 + mblocks * batch - 1) / (mblocks * batch);
-        per = per < cap ? per : cap;
-        per = per < 1 ? 1 : per;
-        const dim3 grid(per, mblocks, batch);
-        hipStream_t st = as_stream(stream);
-        const int ks = Dk / 2 <= 32 ? 32 : (Dk / 2 <= 48 ? 48 : (Dk / 2 <= 64 ? 64 : 0));
-        const bool stream_x = env_variant("RMD_DAP_STREAM") != 0;     // diagnostic: force the KS = 0 form
-#define RMD_DAP(MT, KS)                                                                                     \
-        do {                                                                                                \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_blk_kernel<MT, KS>),          \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-            dap_mfma_blk_kernel<MT, KS><<<grid, kThreads, lds, st>>>(x, weight, disp, pixels, transpose, out); \
-        } while (0)
-        if (ks == 32 && !stream_x) {
-            if (mt == 1) RMD_DAP(1, 32); else RMD_DAP(2, 32);
-        } else if (ks == 48 && !stream_x) {
-            if (mt == 2) RMD_DAP(2, 48); else RMD_DAP(3, 48);
-        } else if (ks == 64 && !stream_x) {
-            if (mt == 3) RMD_DAP(3, 64); else RMD_DAP(4, 64);
-        } else {
-            switch (mt) {
-                case 1: RMD_DAP(1, 0); break;
-                case 2: RMD_DAP(2, 0); break;
-                case 3: RMD_DAP(3, 0); break;
-                default: RMD_DAP(4, 0); break;
-            }
-        }
-#undef RMD_DAP
-        return check_launch("rmd_dap/mfma");
-    }
-    if (disp <= 1024 && env_variant("RMD_DAP_VALU") == 1) {       // round-1 exact-f32 MFMA form
-        const int Dk = (disp + 1) & ~1;
-        const size_t lds = sizeof(float) * 32 * (size_t)(Dk + 1);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dap_mfma_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        dim3 grid((pixels + 127) / 128, (disp + 31) / 32, batch);
-        dap_mfma_kernel<<<grid, kThreads, lds, as_stream(stream)>>>(x, weight, disp, pixels, transpose, out);
-        return check_launch("rmd_dap/mfma");
-    }
-#endif
     const int Kp = (disp + 15) & ~15;
-    if (disp <= 1024 && (long long)(Kp + 16) * pixels * 4 < (1ll << 31) && env_variant("RMD_DAP_VALU") == 0) {
+    if (disp <= 1024 && (long long)(Kp + 16) * pixels * 4 < (1ll << 31)) {
         // split-bf16 MFMA form: M-block of MT row tiles = the largest (<= 4) whose hi / lo W rows fit in
         // 160 KB of LDS; 8 waves per workgroup when the block leaves room for only one workgroup per CU
         const int mt_all = (disp + 31) / 32;
         const size_t rowb = 2 * (size_t)(2 * Kp + 16);       // hi + lo bytes per W row
         int mt = mt_all < 4 ? mt_all : 4;
         while (mt > 1 && (size_t)32 * mt * rowb > 160 * 1024) --mt;
-        mt = std::min(mt, std::max(1, env_knob("RMD_DAP_MT", 4)));          // diagnostic: smaller M-blocks
         const size_t lds = (size_t)32 * mt * rowb;
-        const int nw = env_knob("RMD_DAP_NW", 8) == 4 ? 4 : 8;      // diagnostic: 4-wave workgroups
+        constexpr int nw = 8;
         const int mblocks = (mt_all + mt - 1) / mt;
         const int ntile = (pixels + 31) / 32;
         // one round of workgroups over the chip: ~256 x (workgroups per CU) in all, at least one
         // 32-pixel tile per wave.  At 171-227 VGPRs a SIMD holds 2 waves, so a CU holds one 8-wave
         // workgroup (measured against 4-wave workgroups, 2-3 per CU: 11.5 vs 13.2 us at D = 49, 13.1 vs
         // 15.1 at D = 81, 62 vs 87 at D = 324 — fewer W stagings; profiles/dap_ab_r02.json)
-        const int occ = nw == 8 ? 1 : std::max(1, std::min(3, (int)((160 * 1024) / lds)));
+        const int occ = 1;
         const long long units = (long long)mblocks * batch;
         int per = (int)std::min<long long>((256LL * occ + units - 1) / units, (ntile + nw - 1) / nw);
         per = std::max(per, 1);
@@ -2337,45 +1840,14 @@ extern "C" int rmd_dap(const float* x, const float* weight, int batch, int disp,
             dap_x3_kernel<MT, NW, AUX, KC, NB><<<(unsigned)nwg, NW * 64, lds, st>>>(x, weight, disp, pixels, \
                                                                                   transpose, mblocks, per, out); \
         } while (0)
-#ifdef RMD_DIAG
-        const int dap_nt = env_knob("RMD_DAP_NT", kDapStoreAux);              // diagnostic: store policy
-        const int dap_ring = env_knob("RMD_DAP_RING", 0);                     // diagnostic: x ring shape
-#define RMD_DAPX3_A(MT, NW, AUX)                                                                            \
-        do {                                                                                                \
-            switch (dap_ring) {                                                                             \
-                case 1: RMD_DAPX3_R(MT, NW, AUX, 4, 3); break;                                              \
-                case 2: RMD_DAPX3_R(MT, NW, AUX, 4, 4); break;                                              \
-                case 3: RMD_DAPX3_R(MT, NW, AUX, 2, 8); break;                                              \
-                default: RMD_DAPX3_R(MT, NW, AUX, kDapKC, kDapNB); break;                                  \
-            }                                                                                               \
-        } while (0)
-#define RMD_DAPX3(MT, NW)                                                                                   \
-        do {                                                                                                \
-            if (dap_nt == 2) RMD_DAPX3_A(MT, NW, 2); else RMD_DAPX3_A(MT, NW, 0);                           \
-        } while (0)
-#else
 #define RMD_DAPX3(MT, NW) RMD_DAPX3_R(MT, NW, kDapStoreAux, kDapKC, kDapNB)
-#endif
-        if (nw == 8) {
-            switch (mt) {
-                case 1: RMD_DAPX3(1, 8); break;
-                case 2: RMD_DAPX3(2, 8); break;
-                case 3: RMD_DAPX3(3, 8); break;
-                default: RMD_DAPX3(4, 8); break;
-            }
+        switch (mt) {
+            case 1: RMD_DAPX3(1, 8); break;
+            case 2: RMD_DAPX3(2, 8); break;
+            case 3: RMD_DAPX3(3, 8); break;
+            default: RMD_DAPX3(4, 8); break;
         }
-#ifdef RMD_DIAG
-        else {
-            switch (mt) {
-                case 1: RMD_DAPX3(1, 4); break;
-                case 2: RMD_DAPX3(2, 4); break;
-                case 3: RMD_DAPX3(3, 4); break;
-                default: RMD_DAPX3(4, 4); break;
-            }
-        }
-#endif
 #undef RMD_DAPX3
-#undef RMD_DAPX3_A
 #undef RMD_DAPX3_R
         return check_launch("rmd_dap/x3");
     }

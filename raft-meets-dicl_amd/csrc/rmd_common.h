@@ -103,24 +103,6 @@ __device__ __forceinline__ int xcd_block(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-// Diagnostic variant selector for A/B runs.  Only the diagnostic build (`make diag` ->
-// librmd_diag.so, -DRMD_DIAG; tools/ A/B scripts load it through RMD_LIBRARY) reads the
-// environment (RMD_<NAME>, default 0) and compiles the variant / ablation kernels; in the product
-// library every selector is the constant 0 and the alternatives are not compiled.
-#ifdef RMD_DIAG
-inline int env_variant(const char* name) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : 0;
-}
-inline int env_knob(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-#else
-constexpr int env_variant(const char*) { return 0; }
-constexpr int env_knob(const char*, int dflt) { return dflt; }
-#endif
-
 // vmcnt on gfx950 (as on every gfx9-family CU) is ONE in-order counter for vector loads AND stores.
 // The GEMM tile loops load the next tile's first B fragments (a register ring) before the current
 // tile's epilogue stores; the compiler's wait before a ring register's first use must then leave the
