@@ -106,3 +106,36 @@ def test_dap_b8_full_size(d, h, w):
     got = y[torch.from_numpy(bi).to(DEV), :, torch.from_numpy(yi).to(DEV), torch.from_numpy(xi).to(DEV)]
     ref = x.astype(np.float64)[bi, :, yi, xi] @ wt[:, :, 0, 0].astype(np.float64).T    # (n, D)
     assert_close_elementwise(got.cpu().numpy(), ref, rtol=5e-5, atol=5e-5 * np.abs(ref).max())
+
+
+def test_cfg2_whole_volume_across_gemm_kernels():
+    """cfg2 (B=8, 55x128, C=256) whole volume, every level and a whole lookup output, across three
+    independent GEMM kernels (each pinned to the oracle on samples in test_gpu_corr.py):
+      * fp32 parity mode (corr_pyramid_x3, split-bf16 MFMA, row layout) vs fp32-exact
+        (corr_pyramid_tiled, exact f32 MFMA): max|d| / max|ref| <= 1e-4 (north_star fp32 gate);
+      * bf16 perf mode (corr_pyramid_w8, tiles layout, fp16 storage) vs fp32-exact: <= 1e-2.
+    1.3e10 pyramid values per mode are compared on the GPU (no oracle can run at this size)."""
+    import rmd
+    g = torch.Generator(device="cpu").manual_seed(2024)
+    b, c, h, w = 8, 256, 55, 128
+    f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    f2 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    ys, xs = torch.meshgrid(torch.arange(h, dtype=torch.float32), torch.arange(w, dtype=torch.float32), indexing="ij")
+    flow = torch.nn.functional.interpolate(torch.randn(b, 2, 4, 8, generator=g) * 3.0, size=(h, w), mode="bilinear",
+                                           align_corners=True)
+    co = (torch.stack([xs, ys])[None] + flow + torch.randn(b, 2, 1, 1, generator=g) * 4.0).to(DEV)
+    ref = rmd.ops.corr_pyramid(f1, f2, 4, "fp32-exact")
+    out_ref = rmd.ops.corr_lookup(ref, co, 4)
+    for precision, tol, layout in (("fp32", 1e-4, 0), ("bf16", 1e-2, 1)):
+        pyr = rmd.ops.corr_pyramid(f1, f2, 4, precision)
+        assert pyr.desc.layout == layout
+        for i in range(4):
+            a, r = pyr.unpack(i), ref.unpack(i)
+            err = float((a - r).abs().max() / r.abs().max())
+            assert err < tol, f"{precision} level {i}: {err:.3e}"
+            del a, r
+        out = rmd.ops.corr_lookup(pyr, co, 4)
+        err = float((out - out_ref).abs().max() / out_ref.abs().max())
+        assert err < tol, f"{precision} lookup: {err:.3e}"
+        del pyr, out
+        torch.cuda.empty_cache()
