@@ -6,7 +6,7 @@
 //   tiles4x4 : 4x4 chunks (32 B per slot): per row block i and column group tc two 16-B stores per lane
 //              (halves of its own 4x4 accumulator block), slot stride 32 B
 //   rows1x8  : the round-2 row layout (1x8 chunks, two 512-B runs per instruction after the lane swap)
-//   seq      : each wave writes its share as consecutive 1-KiB blocks (upper bound)
+// (a sequential-store reference is tools/hbm_store_bench.hip's seq: 6.3 TB/s)
 // build: hipcc --offload-arch=gfx950 -O3 -o tools/_bin/store_pattern_bench tools/store_pattern_bench.hip
 #include <hip/hip_runtime.h>
 
@@ -62,12 +62,6 @@ __global__ void __launch_bounds__(512, 1) level0_store(unsigned char* __restrict
                     }
                 }
             }
-        } else {                              // sequential 1-KiB blocks per wave, same byte count
-            const size_t per_wave = (size_t)16 * 16 * 16 * 32;           // 16 stores x 1 KiB per tile
-            const size_t wid = ((size_t)blockIdx.x * 8 + wv) * NQT / 8 + qt / 8;
-            for (int k = 0; k < 16; ++k)
-                __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(pyr + (wid * 16 + k) * 1024 + lane * 16) );
-            (void)per_wave;
         }
     }
 }
@@ -98,12 +92,10 @@ int main() {
         fflush(stdout);
     };
     const double b2x4 = (double)B * 28 * 32 * S * 16, b4x4 = (double)B * 14 * 32 * S * 32, brow = (double)B * 55 * 16 * S * 16;
-    const double bseq = (double)grid * 8 * (NQT / 8.0) * 16 * 1024;
     for (int rep = 0; rep < 2; ++rep) {
         run("tiles2x4", level0_store<0>, b2x4);
         run("tiles4x4", level0_store<1>, b4x4);
         run("rows1x8", level0_store<2>, brow);
-        run("seq", level0_store<3>, bseq);
     }
     CK(hipFree(p));
     return 0;
