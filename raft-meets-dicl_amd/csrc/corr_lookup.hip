@@ -65,7 +65,7 @@ __device__ __forceinline__ int floor_div(int a, int d) { return a >= 0 ? a / d :
 
 // Shift NW words (+1 zero word) left by sh elements of T (sh < TW): whole words in log steps, then a
 // half-word for fp16, and extract the K patch values with zero padding outside [0, lw) / bad rows.
-template <typename T, int K, int TW, int NW>
+template <typename T, int K, int TW, int NW, bool MASK = true>
 __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, int xs, int lw, bool row_ok,
                                               float (&v)[K]) {
     constexpr int S = sizeof(T);
@@ -88,7 +88,47 @@ __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, in
     for (int j = 0; j < K; ++j) {
         const float e = word_elem<T>(wd[j / EPW], j % EPW);
         const int col = xs + j;
-        v[j] = (row_ok && col >= 0 && col < lw) ? e : 0.f;
+        v[j] = (!MASK || (row_ok && col >= 0 && col < lw)) ? e : 0.f;
+    }
+}
+
+// ---- buffer loads (BUF): image b's slab of a level as one buffer resource -----------------------
+// A chunk that is not needed, or lies outside the level (row or chunk index out of range), is loaded
+// from offset kOOB >= the slab size: the hardware returns zeros without touching memory, so no select
+// zeroes loaded words and no clamped address re-reads a line.  The host enables BUF when every
+// per-image level slab is below 2^31 bytes.
+constexpr unsigned kOOB = 0x80000000u;
+
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const PyrGeom& g, int L, int b) {
+    const long long per = (long long)g.ty[L] * g.tx[L] * g.slots * g.th[L] * g.tw[L];     // elements per image
+    const T* base = pyr + g.off[L] + (long long)b * per;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane((unsigned)(per * sizeof(T))),
+                                             0x00020000);
+}
+
+template <int NW>
+__device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_rsrc_t rs, unsigned off) {
+    if constexpr (NW == 4) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[i] = (unsigned)v[i];
+    } else if constexpr (NW == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
+        dst[0] = (unsigned)v[0];
+        dst[1] = (unsigned)v[1];
+    } else if constexpr (NW == 1) {
+        dst[0] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW / 4; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * k), 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dst[4 * k + i] = (unsigned)v[i];
+        }
     }
 }
 
@@ -119,6 +159,32 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
     }
     wd[NW] = 0u;
     shift_extract<T, K, TW, NW>(wd, sh, xs, lw, row_ok, v);
+}
+
+// BUF: the (b, level) block of output planes as one buffer; plane offsets go in the instruction's
+// scalar offset and an inactive lane's kOOB offset drops its stores (no branch, no 64-bit addresses)
+struct OutBuf {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff;     // p * 4, or kOOB for an inactive lane
+};
+
+__device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, bool active) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)o_block);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)o_block >> 32));
+    OutBuf r;
+    r.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
+                                             (int)((unsigned)D * D * N * 4u), 0x00020000);
+    r.voff = active ? (unsigned)p * 4u : kOOB;
+    return r;
+}
+
+template <int D>
+__device__ __forceinline__ void emit_row_buf(const OutBuf& ob, int N, int bb, float fy, const float (&hprev)[D],
+                                             const float (&hcur)[D]) {
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(fmaf(fy, hcur[a] - hprev[a], hprev[a])), ob.rs, (int)ob.voff,
+                                              (int)__builtin_amdgcn_readfirstlane((unsigned)((a * D + bb) * N) * 4u), 2);
 }
 
 // Write the part's output rows: vertical interpolation of consecutive horizontally interpolated rows
@@ -162,10 +228,56 @@ __device__ __forceinline__ bool level_setup(const PyrGeom& g, int L, float x, fl
 // PR: output rows per lane.  A window's D = 2R+1 output rows are split over ceil(D/PR) lanes (part =
 // 0, 1, ...), each loading PR+1 patch rows: more waves in flight for the same stores.  Row layout,
 // or a tiles-layout level with 1-row chunks (levels 2-3).
-template <typename T, int R, int L, int PR>
+//
+// BUF (per-image level slabs < 2^31 B): buffer loads, zeros for chunks off the level from kOOB, and
+// per-element padding masks only in waves where some lane's window reaches past the level's right
+// edge (MASK; a chunk there holds padding columns).  Rows off the level are whole chunks off the level.
+template <typename T, int R, int L, int PR, bool MASK>
+__device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, const PyrGeom& g, int slot, int N,
+                                              float fx, float fy, int xs, int ys, const OutBuf& ob, int own0, int bb0) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, KR = PR + 1;
+    constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 elements
+    constexpr int CB = CW * (int)sizeof(T);                         // chunk bytes
+    constexpr int CWW = CB / 4;                                     // chunk words
+    constexpr int NC = (K + CW - 1 + CW - 1) / CW;                  // chunks a row can span
+    const int lh = g.lh[L], lw = g.lw[L], txs = g.tx[L];
+    const unsigned cs = (unsigned)g.slots * CB, rsb = (unsigned)txs * cs;
+    const int tc0 = floor_div(xs, CW);
+    const int sh = xs - tc0 * CW;
+    const unsigned off0 = (unsigned)tc0 * cs + (unsigned)slot * CB;  // wraps for tc0 < 0: used only when valid
+    float hprev[D];
+#pragma unroll
+    for (int jj = 0; jj < KR; ++jj) {
+        const int j = bb0 + jj;
+        const int yy = ys + j;
+        const bool rv = yy >= 0 && yy < lh;
+        const unsigned roff = off0 + (unsigned)yy * rsb;
+        unsigned wd[NC * CWW + 1];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int tc = tc0 + c;
+            const bool valid = rv && tc >= 0 && tc < txs && c * CW < sh + K;
+            unsigned tmp[CWW];
+            buf_words<CWW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB);
+#pragma unroll
+            for (int i = 0; i < CWW; ++i) wd[c * CWW + i] = tmp[i];
+        }
+        wd[NC * CWW] = 0u;
+        float v[K];
+        shift_extract<T, K, CW, NC * CWW, MASK>(wd, sh, xs, lw, true, v);
+        float hcur[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
+        if (jj > 0 && (PR == D || j - 1 >= own0)) emit_row_buf<D>(ob, N, j - 1, fy, hprev, hcur);
+#pragma unroll
+        for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
+    }
+}
+
+template <typename T, int R, int L, int PR, bool BUF>
 __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, const PyrGeom& g, int b, int slot, int N,
                                                   float x, float y, unsigned zmask, float* __restrict__ o,
-                                                  bool active, int part) {
+                                                  const OutBuf& ob, bool active, int part) {
     constexpr int D = 2 * R + 1;
     constexpr int K = 2 * R + 2;
     constexpr int KR = PR + 1;                                      // patch rows this lane loads
@@ -175,6 +287,14 @@ __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, con
     int xs, ys;
     if (!level_setup<R>(g, L, x, y, zmask, o, N, active, own0, PR, fx, fy, xs, ys)) return;
     const int lh = g.lh[L], lw = g.lw[L];
+    if constexpr (BUF) {
+        const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
+        if (__any(xs + K > lw))
+            rows_body_buf<T, R, L, PR, true>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+        else
+            rows_body_buf<T, R, L, PR, false>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+        return;
+    }
     const T* lvl = pyr + g.off[L];
     constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 (tiles layout: only L >= 2)
     const long long chunk_stride = (long long)g.slots * CW;         // next chunk of the same row
@@ -203,22 +323,19 @@ __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, con
 // Tiles-layout level 0/1: 2 x 4 fp16 chunks (16 B: row 0 in words 0-1, row 1 in words 2-3).  The
 // part's KR patch rows [ya, ya + KR) span NCR chunk rows from cr0 = floor(ya / 2); patch row jj sits in
 // chunk row (jj + par) >> 1, half (jj + par) & 1 with par = ya & 1 — per lane, so each row's 2 * NQ
-// words are selected between the two parities.  Unneeded chunk rows / quads re-read a needed one's
-// address (an L2 hit) and are zeroed.
-template <int R, int L, int PR>
-__device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ pyr, const PyrGeom& g, int b, int slot,
-                                                   int N, float x, float y, unsigned zmask, float* __restrict__ o,
-                                                   bool active, int part) {
+// words are selected between the two parities.  BUF: chunks that are not needed or lie off the level
+// load zeros from kOOB; padding (columns past lw, the odd last row of a chunk row) is masked per
+// element only in waves where some lane's window reaches it (MASK).  !BUF: clamped addresses (an L2
+// hit) and selects.
+template <int R, int L, int PR, bool BUF, bool MASK>
+__device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const PyrGeom& g, int b, int slot, int N,
+                                           float fx, float fy, int xs, int ys, float* __restrict__ o, const OutBuf& ob,
+                                           bool active, int own0, int bb0) {
     constexpr int D = 2 * R + 1;
     constexpr int K = 2 * R + 2;
     constexpr int KR = PR + 1;
     constexpr int NCR = KR / 2 + 1;                                 // chunk rows a part can span
     constexpr int NQ = (K + 3 + 3) / 4;                             // quads a patch row can span
-    const int own0 = part * PR;
-    const int bb0 = min(own0, D - PR);
-    float fx, fy;
-    int xs, ys;
-    if (!level_setup<R>(g, L, x, y, zmask, o, N, active, own0, PR, fx, fy, xs, ys)) return;
     const int lh = g.lh[L], lw = g.lw[L];
     const int ya = ys + bb0;
     const int cr0 = floor_div(ya, 2);
@@ -226,26 +343,46 @@ __device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ py
     const int q0 = floor_div(xs, 4);
     const int sh = xs - 4 * q0;                                     // 0 .. 3
     const int tys = g.ty[L], txs = g.tx[L];
-    const int crl = min(max(cr0, 0), tys - 1), ql = min(max(q0, 0), txs - 1);
-    const long long cs = (long long)g.slots * 8;                    // next quad (elements)
-    const __half* base = pyr + g.off[L] + (long long)slot * 8;
-    const long long bq = (long long)b * tys;
 
     unsigned wd[NCR][NQ][4];
+    if constexpr (BUF) {
+        const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
+        const unsigned cs = (unsigned)g.slots * 16u, rsb = (unsigned)txs * cs;
+        const unsigned off00 = (unsigned)(cr0 * txs + q0) * cs + (unsigned)slot * 16u;   // used only when valid
 #pragma unroll
-    for (int cr = 0; cr < NCR; ++cr) {
-        const int crow = cr0 + cr;
-        const bool rneed = crow >= 0 && crow < tys && 2 * cr <= par + KR - 1;
-        const long long rp = (bq + (rneed ? crow : crl)) * txs;
+        for (int cr = 0; cr < NCR; ++cr) {
+            const int crow = cr0 + cr;
+            const bool rneed = crow >= 0 && crow < tys && 2 * cr <= par + KR - 1;
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            const int q = q0 + c;
-            const bool need = rneed && q >= 0 && q < txs && c * 4 < sh + K;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(base + (rp + (need ? q : ql)) * cs);
-            wd[cr][c][0] = need ? v.x : 0u;
-            wd[cr][c][1] = need ? v.y : 0u;
-            wd[cr][c][2] = need ? v.z : 0u;
-            wd[cr][c][3] = need ? v.w : 0u;
+            for (int c = 0; c < NQ; ++c) {
+                const int q = q0 + c;
+                const bool need = rneed && q >= 0 && q < txs && c * 4 < sh + K;
+                unsigned t4[4];
+                buf_words<4>(t4, rs, need ? off00 + (unsigned)cr * rsb + (unsigned)c * cs : kOOB);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) wd[cr][c][i] = t4[i];
+            }
+        }
+    } else {
+        const int crl = min(max(cr0, 0), tys - 1), ql = min(max(q0, 0), txs - 1);
+        const long long cs = (long long)g.slots * 8;                // next quad (elements)
+        const __half* base = pyr + g.off[L] + (long long)slot * 8;
+        const long long bq = (long long)b * tys;
+#pragma unroll
+        for (int cr = 0; cr < NCR; ++cr) {
+            const int crow = cr0 + cr;
+            const bool rneed = crow >= 0 && crow < tys && 2 * cr <= par + KR - 1;
+            const long long rp = (bq + (rneed ? crow : crl)) * txs;
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) {
+                const int q = q0 + c;
+                const bool need = rneed && q >= 0 && q < txs && c * 4 < sh + K;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(base + (rp + (need ? q : ql)) * cs);
+                wd[cr][c][0] = need ? v.x : 0u;
+                wd[cr][c][1] = need ? v.y : 0u;
+                wd[cr][c][2] = need ? v.z : 0u;
+                wd[cr][c][3] = need ? v.w : 0u;
+            }
         }
     }
 
@@ -268,19 +405,42 @@ __device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ py
         }
         rw[2 * NQ] = 0u;
         float v[K];
-        shift_extract<__half, K, 4, 2 * NQ>(rw, sh, xs, lw, row_ok, v);
+        shift_extract<__half, K, 4, 2 * NQ, MASK>(rw, sh, xs, lw, row_ok, v);
         float hcur[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
         const int j = bb0 + jj;
-        if (jj > 0 && active && (PR == D || j - 1 >= own0)) emit_row<D>(o, N, j - 1, fy, hprev, hcur);
+        if (jj > 0 && (PR == D || j - 1 >= own0)) {
+            if constexpr (BUF) emit_row_buf<D>(ob, N, j - 1, fy, hprev, hcur);
+            else if (active) emit_row<D>(o, N, j - 1, fy, hprev, hcur);
+        }
 #pragma unroll
         for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
     }
 }
 
+template <int R, int L, int PR, bool BUF>
+__device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ pyr, const PyrGeom& g, int b, int slot,
+                                                   int N, float x, float y, unsigned zmask, float* __restrict__ o,
+                                                   const OutBuf& ob, bool active, int part) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, KR = PR + 1;
+    const int own0 = part * PR;
+    const int bb0 = min(own0, D - PR);
+    float fx, fy;
+    int xs, ys;
+    if (!level_setup<R>(g, L, x, y, zmask, o, N, active, own0, PR, fx, fy, xs, ys)) return;
+    if constexpr (BUF) {
+        if (__any(xs + K > g.lw[L] || ys + bb0 + KR > g.lh[L]))
+            tiles_body<R, L, PR, true, true>(pyr, g, b, slot, N, fx, fy, xs, ys, o, ob, active, own0, bb0);
+        else
+            tiles_body<R, L, PR, true, false>(pyr, g, b, slot, N, fx, fy, xs, ys, o, ob, active, own0, bb0);
+    } else {
+        tiles_body<R, L, PR, false, true>(pyr, g, b, slot, N, fx, fy, xs, ys, o, ob, active, own0, bb0);
+    }
+}
+
 // grid: (slot blocks of 64, batch, level + levels * part) — one lane per (query slot, level, row part)
-template <typename T, int R, int PR, int LAY>
+template <typename T, int R, int PR, int LAY, bool BUF>
 __global__ void __launch_bounds__(kThreads)
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
@@ -305,20 +465,23 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     const float x = coords[((size_t)b * 2 + 0) * N + p];
     const float y = coords[((size_t)b * 2 + 1) * N + p];
     constexpr int D = 2 * R + 1;
-    float* o = out + ((size_t)b * g.levels + L) * D * D * N + p;
+    float* ob_block = out + ((size_t)b * g.levels + L) * D * D * N;
+    float* o = ob_block + p;
+    OutBuf ob;
+    if constexpr (BUF) ob = out_buf(ob_block, N, D, p, active);
     if constexpr (LAY == RMD_LAYOUT_TILES) {
         switch (L) {
-            case 0: lookup_level_tiles<R, 0, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            case 1: lookup_level_tiles<R, 1, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            case 2: lookup_level_rows<T, R, 2, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            default: lookup_level_rows<T, R, 3, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
+            case 0: lookup_level_tiles<R, 0, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            case 1: lookup_level_tiles<R, 1, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            case 2: lookup_level_rows<T, R, 2, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            default: lookup_level_rows<T, R, 3, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
         }
     } else {
         switch (L) {
-            case 0: lookup_level_rows<T, R, 0, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            case 1: lookup_level_rows<T, R, 1, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            case 2: lookup_level_rows<T, R, 2, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
-            default: lookup_level_rows<T, R, 3, PR>(pyr, g, b, slot, N, x, y, zmask, o, active, part); break;
+            case 0: lookup_level_rows<T, R, 0, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            case 1: lookup_level_rows<T, R, 1, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            case 2: lookup_level_rows<T, R, 2, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
+            default: lookup_level_rows<T, R, 3, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;
         }
     }
 }
@@ -335,9 +498,20 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
     const PyrGeom g = make_geom(d);
     const dim3 grid((g.slots + kThreads - 1) / kThreads, d.batch, d.levels * 3);
     const T* p = reinterpret_cast<const T*>(pyr);
+    // buffer loads need every per-image level slab below 2^31 bytes (kOOB must lie past it); the
+    // pointer path stays for larger pyramids (-DRMD_LOOKUP_BUF=0 forces it for A/B builds)
+#ifndef RMD_LOOKUP_BUF
+#define RMD_LOOKUP_BUF 1
+#endif
+    bool buf = RMD_LOOKUP_BUF != 0;
+    for (int l = 0; l < d.levels; ++l)
+        buf = buf && (double)d.tiles_y[l] * d.tiles_x[l] * d.query_slots * d.tile_h[l] * d.tile_w[l] * sizeof(T) <
+                         2147483648.0;
+    buf = buf && (double)(2 * radius + 1) * (2 * radius + 1) * d.height * d.width * 4.0 < 2147483648.0;   // output block
     switch (radius) {
 #define RMD_CASE(RR) case RR: \
-        corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        if (buf) corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY, true><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        else corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY, false><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
         break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE
