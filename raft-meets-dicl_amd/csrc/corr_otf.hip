@@ -60,6 +60,12 @@ constexpr int kLd = kMaxT + 5;                       // S row stride (spreads qu
 #ifndef RMD_OTF_OCC_X
 #define RMD_OTF_OCC_X 2
 #endif
+#ifndef RMD_OTF_PF_B
+#define RMD_OTF_PF_B 0
+#endif
+#ifndef RMD_OTF_PF_X
+#define RMD_OTF_PF_X 0
+#endif
 #ifndef RMD_OTF_QSX_X
 #define RMD_OTF_QSX_X 1
 #endif
@@ -244,7 +250,7 @@ template <int QSX, int QSY> struct QBlock {
 // run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC>
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool PF>
 __global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
@@ -366,7 +372,36 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     return tlev + ((size_t)(ry0 + task / nseg) * g.nsx[L] + sa + task % nseg) * segsz +
                            (size_t)lane * SG::LE;
                 };
-                if constexpr (CPT > 0) {
+                if constexpr (CPT > 0 && PF) {
+                    // the next task's target fragments load while this task's MFMAs run (two register
+                    // sets, the loop unrolled by two so the sets alternate without copies)
+                    auto tload = [&](frag (&t)[NLS], int task) {
+                        const T* tsb = tptr(task);
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                    };
+                    auto tmma = [&](const frag (&t)[NLS], int task) {
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) {
+                            f32x4 a = {};
+#pragma unroll
+                            for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(a, t + ls, qf[s] + ls);
+                            store(a, s, task);
+                        }
+                    };
+                    frag t0[NLS], t1[NLS];
+                    int task = w;
+                    if (task < ntask) tload(t0, task);
+                    while (task < ntask) {
+                        if (task + kWaves < ntask) tload(t1, task + kWaves);
+                        tmma(t0, task);
+                        task += kWaves;
+                        if (task >= ntask) break;
+                        if (task + kWaves < ntask) tload(t0, task + kWaves);
+                        tmma(t1, task);
+                        task += kWaves;
+                    }
+                } else if constexpr (CPT > 0) {
                     for (int task = w; task < ntask; task += kWaves) {
                         frag tc[NLS];
                         const T* tsb = tptr(task);
@@ -885,7 +920,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
         using QB = QBlock<QX, QY>;                                                                             \
-        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC>;                                                     \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK>;                                                     \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
         const size_t lds = sizeof(float) * QB::kQ * kLd;                                                       \
@@ -916,14 +951,17 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
+        constexpr bool PFK = RMD_OTF_PF_B != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
+        constexpr bool PFK = RMD_OTF_PF_X != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
+        constexpr bool PFK = false;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
 #undef RMD_OTF_R

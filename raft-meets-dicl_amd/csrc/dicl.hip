@@ -1749,15 +1749,29 @@ dap_wgrad_kernel(const float* __restrict__ g, const float* __restrict__ x, int D
         }
 }
 
-// dW[o][i] = sum over splits in order (deterministic)
-__global__ void __launch_bounds__(256)
+// dW[o][i] = the sum over splits (fixed order: deterministic)
+__global__ void __launch_bounds__(512)
 dap_wgrad_reduce(const float* __restrict__ part, int splits, int D, int Dp, float* __restrict__ dw) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= D * D) return;
-    const int o = idx / D, i = idx % D;
+    // 32 consecutive outputs x 16 split groups per 512-thread workgroup: thread (g, i) sums splits
+    // g, g + 16, ... in order, then the 16 group sums are added in fixed order from LDS — the same
+    // result for every launch (deterministic), with D^2 / 32 workgroups and coalesced 128-B reads
+    __shared__ float red[16][33];
+    const int t = threadIdx.x, i32 = t & 31, gsp = t >> 5;
+    const int idx = blockIdx.x * 32 + i32;
+    const bool ok = idx < D * D;
+    const int o = ok ? idx / D : 0, i = ok ? idx % D : 0;
+    const float* pp = part + (size_t)o * Dp + i;
+    const size_t mat = (size_t)Dp * Dp;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += part[((size_t)k * Dp + o) * Dp + i];
-    dw[idx] = s;
+    for (int k = gsp; k < splits; k += 16) s += pp[(size_t)k * mat];
+    red[gsp][i32] = s;
+    __syncthreads();
+    if (gsp == 0 && ok) {
+        float r = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) r += red[g][i32];
+        dw[idx] = r;
+    }
 }
 
 struct WgPlan {
@@ -1801,7 +1815,7 @@ extern "C" int rmd_dap_weight_grad(const float* grad_out, const float* x, int ba
                                                                     w.Dp, part);
     int rc = rmd::check_launch("rmd_dap_weight_grad");
     if (rc) return rc;
-    rmd::dap_wgrad_reduce<<<(disp * disp + 255) / 256, 256, 0, st>>>(part, w.splits, disp, w.Dp, grad_weight);
+    rmd::dap_wgrad_reduce<<<(disp * disp + 31) / 32, 512, 0, st>>>(part, w.splits, disp, w.Dp, grad_weight);
     return rmd::check_launch("rmd_dap_weight_grad reduce");
 }
 
