@@ -226,11 +226,14 @@ def test_dap_full_324_vs_oracle():
 
 @pytest.mark.parametrize("transpose", [False, True])
 @pytest.mark.parametrize("b,d,h,w", [(3, 25, 7, 9), (2, 130, 5, 13), (1, 200, 33, 1), (2, 1, 4, 4),
-                                     (1, 1000, 3, 5), (2, 324, 12, 16)])
+                                     (1, 1000, 3, 5), (2, 324, 12, 16), (3, 258, 17, 29), (2, 336, 6, 7),
+                                     (1, 352, 9, 40), (3, 260, 6, 10), (1, 1000, 4, 9), (2, 132, 20, 20),
+                                     (1, 144, 16, 17)])
 def test_dap_ragged_vs_oracle(b, d, h, w, transpose):
     """rmd_dap's split-bf16 MFMA GEMM at ragged shapes: D not a multiple of 16 or 32, several M-blocks
-    (D = 130, 200: 2 blocks; 324: 4; 1000: 32 one-tile blocks, 8-wave workgroups), pixel counts that are
-    not a multiple of the 32-pixel tile, D = 1; forward and transposed (the input gradient W^T g)."""
+    (D = 130, 132, 144, 200, 258, 260: 2-3 blocks; 324, 336, 352: 4 with a short or full last block;
+    1000: 32 one-tile blocks, 8-wave workgroups), pixel counts that are not a multiple of the 32-pixel
+    tile, D = 1; forward and transposed (the input gradient W^T g)."""
     import rmd  # noqa: F401
     rng = np.random.default_rng(d * 7 + h)
     x = rng.standard_normal((b, d, h, w)).astype(np.float32)
