@@ -219,6 +219,20 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
     }
 }
 
+// A/B knobs (tools/build_variant.sh -D...; the product build uses the defaults): RMD_X3_ABL = the
+// kernel's ABL, RMD_X3_PP = ping-pong phases, RMD_X3_BHOT = 1 reads every B fragment from query tile 0
+// (an L2-resident B stream; wrong results, timing only)
+#ifndef RMD_X3_ABL
+#define RMD_X3_ABL 0
+#endif
+#ifndef RMD_X3_PP
+#define RMD_X3_PP 1
+#endif
+#ifndef RMD_X3_BHOT
+#define RMD_X3_BHOT 0
+#endif
+#define X3_TILE(t) (RMD_X3_BHOT ? (size_t)0 : (size_t)(t) * 8192)
+
 constexpr int kEpiStores = 24;  // buffer stores of one epilogue (23 in the .s), for vmcnt_pad_n
 constexpr int kRing = 8;     // B ring slots (16 % kRing == 0: k-step s of every tile maps to slot s % kRing)
 
@@ -354,8 +368,8 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
         // MFMAs.
         bf16x8 rh[kRing], rl[kRing];
         if (qt < t_hi) {
-            const __bf16* pb = bHi + bb + (size_t)qt * 8192;
-            const __bf16* pbl = bLo + bb + (size_t)qt * 8192;
+            const __bf16* pb = bHi + bb + X3_TILE(qt);
+            const __bf16* pbl = bLo + bb + X3_TILE(qt);
 #pragma unroll
             for (int s = 0; s < kRing - 1; ++s) {
                 rh[s] = *reinterpret_cast<const bf16x8*>(pb + 512 * s);
@@ -383,11 +397,11 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
 #pragma unroll
                             for (int e = 0; e < 16; ++e) acc[ti][e] = (float)(j + ti + e + k);
                     } else {
-                        const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+                        const size_t pn = X3_TILE(min(qn, nqt - 1));
                         bf16x8 a0[8], a1[8];
                         read_a<0>(a0, smem, b0, b1);
-                        ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192,
-                                  bLo + bb + (size_t)qt * 8192, bHi + bb + pn, bLo + bb + pn);
+                        ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + X3_TILE(qt),
+                                  bLo + bb + X3_TILE(qt), bHi + bb + pn, bLo + bb + pn);
                     }
                     __builtin_amdgcn_s_barrier();
                     epilogue(acc, L, min(qt * 32 + j, N - 1), h);
@@ -403,10 +417,10 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
             while (qt < t_hi) {
                 f32x16 acc[4];
                 const int qn = qt + stride;
-                const size_t pn = (size_t)min(qn, nqt - 1) * 8192;
+                const size_t pn = X3_TILE(min(qn, nqt - 1));
                 bf16x8 a0[8], a1[8];
                 read_a<0>(a0, smem, b0, b1);
-                ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + (size_t)qt * 8192, bLo + bb + (size_t)qt * 8192,
+                ksteps<0>(acc, a0, a1, rh, rl, smem, b0, b1, bHi + bb + X3_TILE(qt), bLo + bb + X3_TILE(qt),
                           bHi + bb + pn, bLo + bb + pn);
                 epilogue(acc, L, min(qt * 32 + j, N - 1), h);
                 qt = qn;
@@ -484,7 +498,7 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const int nwg = (int)(units < ncu ? units : (quarters == 1 ? units : ncu));
     const int lds = kBlockRows * kBlockCols * kRow;
     // ping-pong phases (free-running waves measured slower, profiles/x3_ab_r02.json)
-    auto kern = corr_pyramid_x3<true>;
+    auto kern = corr_pyramid_x3<RMD_X3_PP != 0, RMD_X3_ABL>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     kern<<<nwg, 512, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), (int)units, quarters, tq, reinterpret_cast<float*>(pyr));
     return check_launch("rmd_corr_pyramid/gemm-x3");
