@@ -917,14 +917,25 @@ corr_pyramid_w8(const __bf16* __restrict__ opA, const __bf16* __restrict__ opB, 
     const int j = lane & 31, h = lane >> 5;
 
     const __bf16* gA = opA + (size_t)b * N * Cp;
-    for (int id = tid; id < 256 * CPR; id += 64 * WAVES) {
+    // 16 pieces per thread, all loads in flight before the first LDS store (a load-store loop pays one
+    // HBM round trip per piece before the first MFMA)
+    constexpr int kPieces = 256 * CPR / (64 * WAVES);
+    uint4 av[kPieces];
+#pragma unroll
+    for (int i = 0; i < kPieces; ++i) {
+        const int id = tid + i * 64 * WAVES;
         const int row = id / CPR, c = id - row * CPR;
         // virtual row y >= 8 of a paired block = row y - 8 of the next column block
         const bool second = paired && (row >> 4) >= 8;
         const int ty = ty0 + (row >> 4) - (second ? 8 : 0), tx = tx0 + (row & 15) + (second ? 16 : 0);
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
-        *reinterpret_cast<uint4*>(smem + (size_t)w8::pad_row(row >> 4, row & 15) * w8::kPadRow + c * 16) = v;
+        av[i] = make_uint4(0, 0, 0, 0);
+        if (ty < H && tx < W) av[i] = *reinterpret_cast<const uint4*>(gA + (size_t)(ty * W + tx) * Cp + c * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < kPieces; ++i) {
+        const int id = tid + i * 64 * WAVES;
+        const int row = id / CPR, c = id - row * CPR;
+        *reinterpret_cast<uint4*>(smem + (size_t)w8::pad_row(row >> 4, row & 15) * w8::kPadRow + c * 16) = av[i];
     }
     __syncthreads();
 

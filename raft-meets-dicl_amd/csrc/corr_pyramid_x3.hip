@@ -320,14 +320,24 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
         // ---- A block (hi and lo) -> LDS, zero rows for targets outside the image ----------------
         __syncthreads();                                // the previous unit's fragment reads are done
         const size_t abase = (size_t)b * N * 256;
-        for (int id = tid; id < kBlockRows * kBlockCols * 64; id += 64 * WAVES) {
+        // 16 pieces per thread, all 16 loads in flight before the first LDS store (a load-store loop
+        // pays one HBM round trip per piece: ~16 latencies before the first MFMA)
+        constexpr int kPieces = kBlockRows * kBlockCols * 64 / (64 * WAVES);
+        uint4 v[kPieces];
+#pragma unroll
+        for (int i = 0; i < kPieces; ++i) {
+            const int id = tid + i * 64 * WAVES;
             const int row = id >> 6, c = id & 63;                 // c < 32: hi chunk c, else lo chunk c - 32
-            const int y = row >> 4, x = row & 15;
-            const int ty = ty0 + y, tx = tx0 + x;
-            uint4 v = make_uint4(0, 0, 0, 0);
+            const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
             const __bf16* src = c < 32 ? aHi : aLo;
-            if (ty < H && tx < W) v = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
-            *reinterpret_cast<uint4*>(smem + (size_t)lds_row(y, x) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v;
+            v[i] = make_uint4(0, 0, 0, 0);
+            if (ty < H && tx < W) v[i] = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < kPieces; ++i) {
+            const int id = tid + i * 64 * WAVES;
+            const int row = id >> 6, c = id & 63;
+            *reinterpret_cast<uint4*>(smem + (size_t)lds_row(row >> 4, row & 15) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v[i];
         }
         __syncthreads();
 

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 R=gpurun_out/r03j
 mkdir -p $R
 rm -f $R/x3_ab.jsonl
-run() { RMD_LIBRARY=$1 timeout -k 10 120 python3 -u tools/x3_time.py 20 >> $R/x3_ab.jsonl 2>> $R/err.log; }
+run() { RMD_LIBRARY=$1 timeout -k 10 120 python3 -u tools/x3_time.py ${REPS:-20} ${PREC:-fp32} >> $R/x3_ab.jsonl 2>> $R/err.log; }
 P=$PWD/raft-meets-dicl_amd/rmd/librmd.so
 B=$PWD/tools/_bin
 run $P || exit 3
