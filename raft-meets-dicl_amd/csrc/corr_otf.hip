@@ -18,14 +18,15 @@
 // relative; same split as the fp32-mode GEMM), in the workspace bytes of f32 operands.  RMD_F32 keeps
 // the exact f32 MFMA (fp32-exact).
 //
-// Lookup: one 256-thread block per (query block of 16 x 1 (bf16) / 16 x 2 (fp32 modes) pixels, batch),
-// looping over the levels.  The block's queries' (2r+2)^2 integer patches at level l are bounded by one box (clipped to the map, widened to whole segments),
-// processed in bands of whole rows of at most kMaxT targets: S = band targets x queries, one 16x16
-// MFMA tile per (target segment, query segment), into LDS.  Each (query, x-offset) thread keeps its
-// window rows x-interpolated in registers across bands and finally y-interpolates exactly as
-// rmd_corr_lookup does (shared bilinear weights, zero padding per tap, NaN for 1-pixel levels, zeroed
-// masked levels).  A box wider than kMaxT (flow differing by hundreds of pixels inside one block)
-// takes a per-query VALU patch path.
+// Lookup: one 256-thread block per (query block of QSX x QSY segments of 16 x 1 pixels, batch), looping
+// over the levels.  The block's queries' (2r+2)^2 integer patches at level l are bounded by one box
+// (clipped to the map, widened to whole segments); every (box row, target segment) is one task: one
+// 16x16 MFMA tile per query segment (16 targets x 16 queries), of whose products each lane keeps only
+// those inside its query's own patch, in an LDS patch buffer per query (zero for targets off the map:
+// zero padding per tap).  Each (query, x-offset) thread then interpolates its window exactly as
+// rmd_corr_lookup does (shared bilinear weights, NaN for 1-pixel levels, zeroed masked levels).  A box
+// of more than kMaxTasks segments (flow differing by hundreds of pixels inside one block) takes a
+// per-query VALU patch path.
 #include "rmd_common.h"
 
 #include <algorithm>
@@ -35,8 +36,7 @@ namespace {
 
 constexpr int kThreads = 256;                        // prepare kernels
 constexpr int kLookThreads = 256, kWaves = kLookThreads / 64;
-constexpr int kMaxT = 384;                           // targets of one band
-constexpr int kLd = kMaxT + 5;                       // S row stride (spreads queries over banks)
+constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block and occupancy per compute (-D knobs for A/B builds, tools/_gpu_r03c.sh).  cfg2, one box
 // (profiles/otf_block_ab_r03.json): bf16 16x1 blocks at 2 workgroups per CU 90 us vs 16x2 at one 112 us
 // (16x4: 147, 32x1: 103 — larger boxes waste MFMA tiles and cut the number of blocks in flight; the
@@ -62,6 +62,10 @@ constexpr int kLd = kMaxT + 5;                       // S row stride (spreads qu
 #endif
 #ifndef RMD_OTF_PF_B
 #define RMD_OTF_PF_B 0
+#endif
+// ablations for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks
+#ifndef RMD_OTF_ABL
+#define RMD_OTF_ABL 0
 #endif
 #ifndef RMD_OTF_PF_X
 #define RMD_OTF_PF_X 0
@@ -258,8 +262,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     using frag = typename SG::frag;
     using QB = QBlock<QSX, QSY>;
     constexpr int kQS = QB::kQS, kBX = QB::kBX, kBY = QB::kBY, kQ = QB::kQ;
-    constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K;
-    extern __shared__ float S[];                       // [kQ][kLd]: band (boxed) or patch (per query)
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = KK + 1;   // odd patch stride: queries spread over banks
+    extern __shared__ float S[];                       // [kQ][KKp]: every query's (2r+2)^2 patch
     // every level's window origins / fractions and the block's bounding box per level, computed once
     // before the level loop (no per-level reduction barriers)
     __shared__ int box[RMD_MAX_LEVELS][4];             // x0, x1, y0, y1 (min / max)
@@ -284,29 +288,18 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
         qsb[s] = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + s / QSX, g.H - 1) * g.qnsx +
                          min((qx0 >> 4) + s % QSX, g.qnsx - 1)) * segsz;
 
-    // the block's query segments (CPT > 0): one coalesced copy into LDS, overlapping the coords
-    // load; each wave then keeps its register fragments for every level and target segment
+    // the block's query fragments (CPT > 0): each wave keeps them in registers for every level and
+    // target segment (a load step is one coalesced 1-KiB read per instruction)
     constexpr int NLS = CPT > 0 ? CPT / SG::LSC * NP : 1;                 // load steps per segment
-    constexpr int QV = CPT > 0 ? 16 * CPT * NP * (int)sizeof(T) / 16 : 0;     // 16-B vectors per segment
-    static_assert(kQS * QV * 16 <= kQ * kLd * 4, "the query segments must fit the S buffer");
-    if constexpr (CPT > 0) {
-        uint4* dst = reinterpret_cast<uint4*>(S);
-#pragma unroll
-        for (int s = 0; s < kQS; ++s) {
-            const uint4* src = reinterpret_cast<const uint4*>(qsb[s]);
-            for (int v = tid; v < QV; v += kLookThreads) dst[s * QV + v] = src[v];
-        }
-    }
-    if (tid < RMD_MAX_LEVELS * 4) box[tid >> 2][tid & 3] = (tid & 1) ? -(1 << 30) : (1 << 30);
-    __syncthreads();
     frag qf[kQS][NLS];
     if constexpr (CPT > 0) {
-        const frag* qs = reinterpret_cast<const frag*>(S);
 #pragma unroll
         for (int s = 0; s < kQS; ++s)
 #pragma unroll
-            for (int ls = 0; ls < NLS; ++ls) qf[s][ls] = qs[(s * NLS + ls) * 64 + lane];
+            for (int ls = 0; ls < NLS; ++ls) qf[s][ls] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)ls * 64 + lane) * SG::LE);
     }
+    if (tid < RMD_MAX_LEVELS * 4) box[tid >> 2][tid & 3] = (tid & 1) ? -(1 << 30) : (1 << 30);
+    __syncthreads();
     // thread (level, query) items: every level's window origin (coords clamped as rmd_corr_lookup does)
     for (int it = tid; it < kQ * g.L; it += kLookThreads) {
         const int q = it % kQ, L = it / kQ;
@@ -328,7 +321,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
         atomicMin(&box[L][2], ys);
         atomicMax(&box[L][3], ys + K - 1);
     }
-    __syncthreads();                                   // boxes complete; the query fragments are read: S is free
+    __syncthreads();                                   // boxes complete
     // thread items (q, a): query q, window x-offset a; hx[i][jj] = row jj of the window, x-interpolated
     constexpr int ITEMS = (kQ * D + kLookThreads - 1) / kLookThreads;
 
@@ -349,7 +342,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
         const int bx0 = max(box[L][0], 0), bx1 = min(box[L][1], lw - 1);
         const int by0 = max(box[L][2], 0), by1 = min(box[L][3], lh - 1);
         const int th = max(by1 - by0 + 1, 0);
-        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0, sw = nseg * 16;
+        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0;
+        const int ntask = th * nseg;                   // (box row, target segment) MFMA tasks
         const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
 
         float hx[ITEMS][K];
@@ -358,113 +352,116 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
 #pragma unroll
             for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
 
-        if (sw <= kMaxT) {
-            const int bh = sw > 0 ? kMaxT / sw : 1;
-            for (int ry0 = by0; ry0 < by0 + th; ry0 += bh) {
-                const int nrow = min(bh, by0 + th - ry0), ntask = nrow * nseg;
-                // C[target 4*(lane>>4)+e][query lane&15] -> S[query][band target]
-                auto store = [&](const f32x4& a, int s, int task) {
-                    const int col = (task / nseg) * sw + (task % nseg) * 16 + 4 * (lane >> 4), j = lane & 15;
+        if (RMD_OTF_ABL != 2 && ntask > 0 && ntask <= kMaxTasks) {
+            // every query's (2r+2)^2 patch in LDS, zero where the target is off the map (zero padding)
+            for (int i = tid; i < kQ * KKp; i += kLookThreads) S[i] = 0.f;
+            // the lane's query in each query segment: its window origin at this level
+            int wx[kQS], wy[kQS], wq[kQS];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) S[(s * 16 + j) * kLd + col + e] = a[e];
-                };
-                auto tptr = [&](int task) {
-                    return tlev + ((size_t)(ry0 + task / nseg) * g.nsx[L] + sa + task % nseg) * segsz +
-                           (size_t)lane * SG::LE;
-                };
-                if constexpr (CPT > 0 && PF) {
-                    // the next task's target fragments load while this task's MFMAs run (two register
-                    // sets, the loop unrolled by two so the sets alternate without copies)
-                    auto tload = [&](frag (&t)[NLS], int task) {
-                        const T* tsb = tptr(task);
-#pragma unroll
-                        for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-                    };
-                    auto tmma = [&](const frag (&t)[NLS], int task) {
-#pragma unroll
-                        for (int s = 0; s < kQS; ++s) {
-                            f32x4 a = {};
-#pragma unroll
-                            for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(a, t + ls, qf[s] + ls);
-                            store(a, s, task);
-                        }
-                    };
-                    frag t0[NLS], t1[NLS];
-                    int task = w;
-                    if (task < ntask) tload(t0, task);
-                    while (task < ntask) {
-                        if (task + kWaves < ntask) tload(t1, task + kWaves);
-                        tmma(t0, task);
-                        task += kWaves;
-                        if (task >= ntask) break;
-                        if (task + kWaves < ntask) tload(t0, task + kWaves);
-                        tmma(t1, task);
-                        task += kWaves;
-                    }
-                } else if constexpr (CPT > 0) {
-                    for (int task = w; task < ntask; task += kWaves) {
-                        frag tc[NLS];
-                        const T* tsb = tptr(task);
-#pragma unroll
-                        for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-#pragma unroll
-                        for (int s = 0; s < kQS; ++s) {
-                            f32x4 a = {};
-#pragma unroll
-                            for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(a, tc + ls, qf[s] + ls);
-                            store(a, s, task);
-                        }
-                    }
-                } else {
-                    for (int task = w; task < ntask; task += kWaves) {
-                        const T* tsb = tptr(task);
-                        f32x4 a[kQS];
-#pragma unroll
-                        for (int s = 0; s < kQS; ++s) a[s] = f32x4{};
-                        for (int ls = 0; ls < nls * NP; ls += NP) {
-                            frag t[NP];
-#pragma unroll
-                            for (int p = 0; p < NP; ++p) t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
-#pragma unroll
-                            for (int s = 0; s < kQS; ++s) {
-                                frag u[NP];
-#pragma unroll
-                                for (int p = 0; p < NP; ++p)
-                                    u[p] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)(ls + p) * 64 + lane) * SG::LE);
-                                seg_mma<T, X3>(a[s], t, u);
-                            }
-                        }
-#pragma unroll
-                        for (int s = 0; s < kQS; ++s) store(a[s], s, task);
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < ITEMS; ++i) {
-                    const int idx = tid + i * kLookThreads;
-                    if (idx >= kQ * D) break;
-                    const int q = idx % kQ, a = idx / kQ;
-                    const int xs = sxs[L][q], ys = sys[L][q];
-                    const float fx = sfx[L][q];
-                    const float* Sq = S + q * kLd;
-#pragma unroll
-                    for (int jj = 0; jj < K; ++jj) {
-                        const int ty = ys + jj;
-                        if (ty >= ry0 && ty < ry0 + nrow) {
-                            float v[2];
-#pragma unroll
-                            for (int u = 0; u < 2; ++u) {
-                                const int tx = xs + a + u;
-                                v[u] = (tx >= 0 && tx < lw) ? Sq[(ty - ry0) * sw + (tx - sa * 16)] : 0.f;
-                            }
-                            hx[i][jj] = fmaf(fx, v[1] - v[0], v[0]);
-                        }
-                    }
-                }
-                __syncthreads();
+            for (int s = 0; s < kQS; ++s) {
+                wq[s] = (s / QSX) * kBX + (s % QSX) * 16 + (lane & 15);
+                wx[s] = sxs[L][wq[s]];
+                wy[s] = sys[L][wq[s]];
             }
-        } else {
-            // box wider than kMaxT: each query's own (2r+2)^2 patch, one dot product per thread
+            __syncthreads();
+            // C[target 4*(lane>>4)+e][query lane&15] of task (box row, segment): keep the products inside
+            // the query's own patch
+            auto put = [&](const f32x4& acc, int s, int task) {
+                const int r = task / nseg;
+                const int dy = by0 + r - wy[s];
+                const int dx0 = (sa + task - r * nseg) * 16 + 4 * (lane >> 4) - wx[s];
+                if ((unsigned)dy < (unsigned)K) {
+                    float* P = S + wq[s] * KKp + dy * K;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if ((unsigned)(dx0 + e) < (unsigned)K) P[dx0 + e] = acc[e];
+                }
+            };
+            auto tptr = [&](int task) {
+                const int r = task / nseg;
+                return tlev + ((size_t)(by0 + r) * g.nsx[L] + sa + task - r * nseg) * segsz + (size_t)lane * SG::LE;
+            };
+            if constexpr (CPT > 0 && PF) {
+                // the next task's target fragments load while this task's MFMAs run (two register sets,
+                // the loop unrolled by two so the sets alternate without copies)
+                auto tload = [&](frag (&t)[NLS], int task) {
+                    const T* tsb = tptr(task);
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                };
+                auto tmma = [&](const frag (&t)[NLS], int task) {
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) {
+                        f32x4 acc = {};
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(acc, t + ls, qf[s] + ls);
+                        put(acc, s, task);
+                    }
+                };
+                frag t0[NLS], t1[NLS];
+                int task = w;
+                if (task < ntask) tload(t0, task);
+                while (task < ntask) {
+                    if (task + kWaves < ntask) tload(t1, task + kWaves);
+                    tmma(t0, task);
+                    task += kWaves;
+                    if (task >= ntask) break;
+                    if (task + kWaves < ntask) tload(t0, task + kWaves);
+                    tmma(t1, task);
+                    task += kWaves;
+                }
+            } else if constexpr (CPT > 0) {
+                for (int task = w; task < ntask; task += kWaves) {
+                    frag tc[NLS];
+                    const T* tsb = tptr(task);
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) {
+                        f32x4 acc = {};
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(acc, tc + ls, qf[s] + ls);
+                        put(acc, s, task);
+                    }
+                }
+            } else {
+                for (int task = w; task < ntask; task += kWaves) {
+                    const T* tsb = tptr(task);
+                    f32x4 acc[kQS];
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) acc[s] = f32x4{};
+                    for (int ls = 0; ls < nls * NP; ls += NP) {
+                        frag t[NP];
+#pragma unroll
+                        for (int p = 0; p < NP; ++p) t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) {
+                            frag u[NP];
+#pragma unroll
+                            for (int p = 0; p < NP; ++p)
+                                u[p] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                            seg_mma<T, X3>(acc[s], t, u);
+                        }
+                    }
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) put(acc[s], s, task);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const int idx = tid + i * kLookThreads;
+                if (idx >= kQ * D) break;
+                const int q = idx % kQ, a = idx / kQ;
+                const float fx = sfx[L][q];
+                const float* P = S + q * KKp + a;
+#pragma unroll
+                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, P[jj * K + 1] - P[jj * K], P[jj * K]);
+            }
+            __syncthreads();                           // S is free for the next level
+        } else if (ntask > 0) {
+            // a box of more than kMaxTasks segments (flow differing by hundreds of pixels inside one
+            // block): each query's own (2r+2)^2 patch, one dot product per thread
             for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
                 const int q = idx / KK, r = idx - q * KK;
                 const int ty = sys[L][q] + r / K, tx = sxs[L][q] + r % K;
@@ -476,7 +473,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     for (int c = 0; c < g.C; ++c)
                         acc = fmaf(seg_elem<T, X3>(qs, qc % 16, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
                 }
-                S[q * kLd + r] = acc;
+                S[q * KKp + r] = acc;
             }
             __syncthreads();
 #pragma unroll
@@ -485,9 +482,9 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 if (idx >= kQ * D) break;
                 const int q = idx % kQ, a = idx / kQ;
                 const float fx = sfx[L][q];
-                const float* Sq = S + q * kLd;
+                const float* P = S + q * KKp + a;
 #pragma unroll
-                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Sq[jj * K + a + 1] - Sq[jj * K + a], Sq[jj * K + a]);
+                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, P[jj * K + 1] - P[jj * K], P[jj * K]);
             }
             __syncthreads();                           // S is free for the next level
         }
@@ -501,6 +498,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y >= g.H || x >= g.W) continue;
             const float fy = sfy[L][q] + (sfx[L][q] - sfx[L][q]);   // a NaN x weight reaches rows outside the band too
+            if (RMD_OTF_ABL == 1 && fy != 12345.f) continue;
             float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
             for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
@@ -923,7 +921,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK>;                                                     \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
-        const size_t lds = sizeof(float) * QB::kQ * kLd;                                                       \
+        const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1);                       \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
