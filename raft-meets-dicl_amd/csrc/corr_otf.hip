@@ -35,7 +35,10 @@ namespace rmd {
 namespace {
 
 constexpr int kThreads = 256;                        // prepare kernels
-constexpr int kLookThreads = 256, kWaves = kLookThreads / 64;
+#ifndef RMD_OTF_NT
+#define RMD_OTF_NT 256
+#endif
+constexpr int kLookThreads = RMD_OTF_NT, kWaves = kLookThreads / 64;   // lookup workgroup
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block and occupancy per compute (-D knobs for A/B builds, tools/_gpu_r03c.sh).  cfg2, one box
 // (profiles/otf_block_ab_r03.json): bf16 16x1 blocks at 2 workgroups per CU 90 us vs 16x2 at one 112 us
@@ -62,6 +65,12 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #endif
 #ifndef RMD_OTF_PF_B
 #define RMD_OTF_PF_B 0
+#endif
+#ifndef RMD_OTF_QL_B
+#define RMD_OTF_QL_B 0
+#endif
+#ifndef RMD_OTF_QL_X
+#define RMD_OTF_QL_X 0
 #endif
 // ablations for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks
 #ifndef RMD_OTF_ABL
@@ -254,7 +263,7 @@ template <int QSX, int QSY> struct QBlock {
 // run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool PF>
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool PF, bool QL>
 __global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
@@ -289,15 +298,34 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                          min((qx0 >> 4) + s % QSX, g.qnsx - 1)) * segsz;
 
     // the block's query fragments (CPT > 0): each wave keeps them in registers for every level and
-    // target segment (a load step is one coalesced 1-KiB read per instruction)
+    // target segment (a load step is one coalesced 1-KiB read per instruction), or (QL) one copy in
+    // LDS behind the patch buffers, read per MFMA (fewer VGPRs: more waves and target loads in flight)
     constexpr int NLS = CPT > 0 ? CPT / SG::LSC * NP : 1;                 // load steps per segment
-    frag qf[kQS][NLS];
-    if constexpr (CPT > 0) {
+    constexpr bool QREG = CPT > 0 && !QL;
+    frag qf[QREG ? kQS : 1][QREG ? NLS : 1];
+    const frag* qlds = reinterpret_cast<const frag*>(S + kQ * KKp);
+    if constexpr (QREG) {
 #pragma unroll
         for (int s = 0; s < kQS; ++s)
 #pragma unroll
             for (int ls = 0; ls < NLS; ++ls) qf[s][ls] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)ls * 64 + lane) * SG::LE);
+    } else if constexpr (CPT > 0) {
+        constexpr int QV = 16 * CPT * NP * (int)sizeof(T) / 16;            // 16-B vectors per segment
+        uint4* dst = reinterpret_cast<uint4*>(S + kQ * KKp);
+#pragma unroll
+        for (int s = 0; s < kQS; ++s) {
+            const uint4* src = reinterpret_cast<const uint4*>(qsb[s]);
+            for (int v = tid; v < QV; v += kLookThreads) dst[s * QV + v] = src[v];
+        }
     }
+    // query fragments (s, load steps ls .. ls + NP - 1) of this lane
+    auto qget = [&](frag (&u)[NP], int s, int ls) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if constexpr (QREG) u[p] = qf[s][ls + p];
+            else u[p] = qlds[(s * NLS + ls + p) * 64 + lane];
+        }
+    };
     if (tid < RMD_MAX_LEVELS * 4) box[tid >> 2][tid & 3] = (tid & 1) ? -(1 << 30) : (1 << 30);
     __syncthreads();
     // thread (level, query) items: every level's window origin (coords clamped as rmd_corr_lookup does)
@@ -394,7 +422,11 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     for (int s = 0; s < kQS; ++s) {
                         f32x4 acc = {};
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(acc, t + ls, qf[s] + ls);
+                        for (int ls = 0; ls < NLS; ls += NP) {
+                            frag u[NP];
+                            qget(u, s, ls);
+                            seg_mma<T, X3>(acc, t + ls, u);
+                        }
                         put(acc, s, task);
                     }
                 };
@@ -420,7 +452,11 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                     for (int s = 0; s < kQS; ++s) {
                         f32x4 acc = {};
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ls += NP) seg_mma<T, X3>(acc, tc + ls, qf[s] + ls);
+                        for (int ls = 0; ls < NLS; ls += NP) {
+                            frag u[NP];
+                            qget(u, s, ls);
+                            seg_mma<T, X3>(acc, tc + ls, u);
+                        }
                         put(acc, s, task);
                     }
                 }
@@ -918,10 +954,11 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
         using QB = QBlock<QX, QY>;                                                                             \
-        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK>;                                                     \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK, QLK>;                                        \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
-        const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1);                       \
+        const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +                      \
+                           (QLK && CC > 0 ? (size_t)QB::kQS * 16 * CC * XN * sizeof(T) : 0);                    \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
@@ -950,16 +987,19 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool PFK = RMD_OTF_PF_B != 0;
+        constexpr bool QLK = RMD_OTF_QL_B != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
         constexpr bool PFK = RMD_OTF_PF_X != 0;
+        constexpr bool QLK = RMD_OTF_QL_X != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool PFK = false;
+        constexpr bool QLK = false;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
 #undef RMD_OTF_R
