@@ -49,7 +49,7 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #define RMD_OTF_QSX_B 1
 #endif
 #ifndef RMD_OTF_QSY_B
-#define RMD_OTF_QSY_B 1
+#define RMD_OTF_QSY_B 2
 #endif
 #ifndef RMD_OTF_QSX_X
 #define RMD_OTF_QSX_X 1
@@ -63,8 +63,11 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_OCC_X
 #define RMD_OTF_OCC_X 2
 #endif
+#ifndef RMD_OTF_PF_B
+#define RMD_OTF_PF_B 0
+#endif
 #ifndef RMD_OTF_QL_B
-#define RMD_OTF_QL_B 0
+#define RMD_OTF_QL_B 1
 #endif
 #ifndef RMD_OTF_QL_X
 #define RMD_OTF_QL_X 0
@@ -72,6 +75,9 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 // ablations for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks
 #ifndef RMD_OTF_ABL
 #define RMD_OTF_ABL 0
+#endif
+#ifndef RMD_OTF_PF_X
+#define RMD_OTF_PF_X 0
 #endif
 #ifndef RMD_OTF_QSX_X
 #define RMD_OTF_QSX_X 1
@@ -257,7 +263,7 @@ template <int QSX, int QSY> struct QBlock {
 // run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool QL>
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool PF, bool QL>
 __global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
@@ -266,7 +272,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     using QB = QBlock<QSX, QSY>;
     constexpr int kQS = QB::kQS, kBX = QB::kBX, kBY = QB::kBY, kQ = QB::kQ;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = KK + 1;   // odd patch stride: queries spread over banks
-    extern __shared__ float S[];                       // [L][kQ][KKp]: every query's (2r+2)^2 patches | (QL) query fragments
+    extern __shared__ float S[];                       // [kQ][KKp]: every query's (2r+2)^2 patch
     // every level's window origins / fractions and the block's bounding box per level, computed once
     // before the level loop (no per-level reduction barriers)
     __shared__ int box[RMD_MAX_LEVELS][4];             // x0, x1, y0, y1 (min / max)
@@ -297,7 +303,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     constexpr int NLS = CPT > 0 ? CPT / SG::LSC * NP : 1;                 // load steps per segment
     constexpr bool QREG = CPT > 0 && !QL;
     frag qf[QREG ? kQS : 1][QREG ? NLS : 1];
-    const frag* qlds = reinterpret_cast<const frag*>(S + g.L * kQ * KKp);
+    const frag* qlds = reinterpret_cast<const frag*>(S + kQ * KKp);
     if constexpr (QREG) {
 #pragma unroll
         for (int s = 0; s < kQS; ++s)
@@ -305,7 +311,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             for (int ls = 0; ls < NLS; ++ls) qf[s][ls] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)ls * 64 + lane) * SG::LE);
     } else if constexpr (CPT > 0) {
         constexpr int QV = 16 * CPT * NP * (int)sizeof(T) / 16;            // 16-B vectors per segment
-        uint4* dst = reinterpret_cast<uint4*>(S + g.L * kQ * KKp);
+        uint4* dst = reinterpret_cast<uint4*>(S + kQ * KKp);
 #pragma unroll
         for (int s = 0; s < kQS; ++s) {
             const uint4* src = reinterpret_cast<const uint4*>(qsb[s]);
@@ -346,152 +352,13 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     __syncthreads();                                   // boxes complete
     // thread items (q, a): query q, window x-offset a; hx[i][jj] = row jj of the window, x-interpolated
     constexpr int ITEMS = (kQ * D + kLookThreads - 1) / kLookThreads;
-    constexpr int LP = kQ * KKp;                       // patch floats per level
-    // per level (wave-uniform): the box's first row and first target segment, its segments per row,
-    // the MFMA tasks (0: masked, degenerate, empty or a box of more than kMaxTasks segments) and
-    // whether the per-query VALU path runs it
-    int lby0[RMD_MAX_LEVELS], lsa[RMD_MAX_LEVELS], lnseg[RMD_MAX_LEVELS], lnt[RMD_MAX_LEVELS];
-    bool lslow[RMD_MAX_LEVELS];
-    int total = 0;
-#pragma unroll
-    for (int L = 0; L < RMD_MAX_LEVELS; ++L) {
-        lby0[L] = 0;
-        lsa[L] = 0;
-        lnseg[L] = 1;
-        lnt[L] = 0;
-        lslow[L] = false;
-        if (L >= g.L) continue;
-        const int lh = g.lh[L], lw = g.lw[L];
-        if (((zmask >> L) & 1u) || lh < 2 || lw < 2) continue;
-        const int bx0 = max(box[L][0], 0), bx1 = min(box[L][1], lw - 1);
-        const int by0 = max(box[L][2], 0), by1 = min(box[L][3], lh - 1);
-        const int th = max(by1 - by0 + 1, 0);
-        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0;
-        const int ntask = th * nseg;                   // (box row, target segment) MFMA tasks
-        lby0[L] = by0;
-        lsa[L] = sa;
-        lnseg[L] = max(nseg, 1);
-        if (ntask <= kMaxTasks) {
-            lnt[L] = ntask;
-            total += ntask;
-        } else {
-            lslow[L] = true;
-        }
-    }
-    auto sel = [](const int (&v)[RMD_MAX_LEVELS], int L) {
-        int r = v[0];
-#pragma unroll
-        for (int k = 1; k < RMD_MAX_LEVELS; ++k)
-            if (L == k) r = v[k];
-        return r;
-    };
-    // every query's (2r+2)^2 patch of every level in LDS, zero where the target is off the map (zero
-    // padding); one task pool over all levels (no per-level barriers, no per-level tail of idle waves)
-    for (int i = tid; i < g.L * LP; i += kLookThreads) S[i] = 0.f;
-    __syncthreads();
-    // task -> (level, box row, target segment); C[target 4*(lane>>4)+e][query lane&15] of query segment s:
-    // keep the products inside the query's own patch
-    auto locate = [&](int task, int& L, int& row, int& col) {
-        int t = task;
-        L = 0;
-#pragma unroll
-        for (int k = 0; k < RMD_MAX_LEVELS - 1; ++k)
-            if (L == k && t >= lnt[k]) {
-                t -= lnt[k];
-                L = k + 1;
-            }
-        const int nseg = sel(lnseg, L);
-        const int r = t / nseg;
-        row = sel(lby0, L) + r;
-        col = sel(lsa, L) + t - r * nseg;
-    };
-    auto put = [&](const f32x4& acc, int s, int L, int row, int col) {
-        const int q = (s / QSX) * kBX + (s % QSX) * 16 + (lane & 15);
-        const int dy = row - sys[L][q];
-        const int dx0 = col * 16 + 4 * (lane >> 4) - sxs[L][q];
-        if ((unsigned)dy < (unsigned)K) {
-            float* P = S + L * LP + q * KKp + dy * K;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if ((unsigned)(dx0 + e) < (unsigned)K) P[dx0 + e] = acc[e];
-        }
-    };
-    auto tptr = [&](int L, int row, int col) {
-        return tseg + ((size_t)b * g.TS + g.soff[L] + (size_t)row * g.nsx[L] + col) * segsz + (size_t)lane * SG::LE;
-    };
-    if constexpr (CPT > 0) {
-        for (int task = w; task < total; task += kWaves) {
-            int L, row, col;
-            locate(task, L, row, col);
-            frag tc[NLS];
-            const T* tsb = tptr(L, row, col);
-#pragma unroll
-            for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-#pragma unroll
-            for (int s = 0; s < kQS; ++s) {
-                f32x4 acc = {};
-#pragma unroll
-                for (int ls = 0; ls < NLS; ls += NP) {
-                    frag u[NP];
-                    qget(u, s, ls);
-                    seg_mma<T, X3>(acc, tc + ls, u);
-                }
-                put(acc, s, L, row, col);
-            }
-        }
-    } else {
-        for (int task = w; task < total; task += kWaves) {
-            int L, row, col;
-            locate(task, L, row, col);
-            const T* tsb = tptr(L, row, col);
-            f32x4 acc[kQS];
-#pragma unroll
-            for (int s = 0; s < kQS; ++s) acc[s] = f32x4{};
-            for (int ls = 0; ls < nls * NP; ls += NP) {
-                frag t[NP];
-#pragma unroll
-                for (int p = 0; p < NP; ++p) t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
-#pragma unroll
-                for (int s = 0; s < kQS; ++s) {
-                    frag u[NP];
-#pragma unroll
-                    for (int p = 0; p < NP; ++p)
-                        u[p] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)(ls + p) * 64 + lane) * SG::LE);
-                    seg_mma<T, X3>(acc[s], t, u);
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < kQS; ++s) put(acc[s], s, L, row, col);
-        }
-    }
-    // a box of more than kMaxTasks segments (flow differing by hundreds of pixels inside one block):
-    // each query's own (2r+2)^2 patch, one dot product per thread
-#pragma unroll
-    for (int L = 0; L < RMD_MAX_LEVELS; ++L) {
-        if (!lslow[L]) continue;
-        const int lh = g.lh[L], lw = g.lw[L];
-        const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
-        for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
-            const int q = idx / KK, r = idx - q * KK;
-            const int ty = sys[L][q] + r / K, tx = sxs[L][q] + r % K;
-            float acc = 0.f;
-            if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
-                const int qr = q / kBX, qc = q % kBX;
-                const T* qs = qsb[qr * QSX + qc / 16];
-                const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
-                for (int c = 0; c < g.C; ++c)
-                    acc = fmaf(seg_elem<T, X3>(qs, qc % 16, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
-            }
-            S[L * LP + q * KKp + r] = acc;
-        }
-    }
-    __syncthreads();
 
     for (int L = 0; L < g.L; ++L) {
+        const int lh = g.lh[L], lw = g.lw[L];
         float* ob = out + ((size_t)b * g.L + L) * D * D * (size_t)N;
         // masked / degenerate level: constant output (raft_fs.py:77-78; 1-pixel levels divide by zero)
         const bool masked = (zmask >> L) & 1u;
-        if (masked || g.lh[L] < 2 || g.lw[L] < 2) {
+        if (masked || lh < 2 || lw < 2) {
             const float v = masked ? 0.f : __builtin_nanf("");
             for (int idx = tid; idx < kQ * D * D; idx += kLookThreads) {
                 const int q = idx % kQ, c = idx / kQ;
@@ -500,7 +367,165 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             }
             continue;
         }
-        // x-interpolation from the patch, y-interpolation and the (a, b)-major output planes
+        const int bx0 = max(box[L][0], 0), bx1 = min(box[L][1], lw - 1);
+        const int by0 = max(box[L][2], 0), by1 = min(box[L][3], lh - 1);
+        const int th = max(by1 - by0 + 1, 0);
+        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0;
+        const int ntask = th * nseg;                   // (box row, target segment) MFMA tasks
+        const T* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
+
+        float hx[ITEMS][K];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
+
+        if (RMD_OTF_ABL != 2 && ntask > 0 && ntask <= kMaxTasks) {
+            // every query's (2r+2)^2 patch in LDS, zero where the target is off the map (zero padding)
+            for (int i = tid; i < kQ * KKp; i += kLookThreads) S[i] = 0.f;
+            // the lane's query in each query segment: its window origin at this level
+            int wx[kQS], wy[kQS], wq[kQS];
+#pragma unroll
+            for (int s = 0; s < kQS; ++s) {
+                wq[s] = (s / QSX) * kBX + (s % QSX) * 16 + (lane & 15);
+                wx[s] = sxs[L][wq[s]];
+                wy[s] = sys[L][wq[s]];
+            }
+            __syncthreads();
+            // C[target 4*(lane>>4)+e][query lane&15] of task (box row, segment): keep the products inside
+            // the query's own patch
+            auto put = [&](const f32x4& acc, int s, int task) {
+                const int r = task / nseg;
+                const int dy = by0 + r - wy[s];
+                const int dx0 = (sa + task - r * nseg) * 16 + 4 * (lane >> 4) - wx[s];
+                if ((unsigned)dy < (unsigned)K) {
+                    float* P = S + wq[s] * KKp + dy * K;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if ((unsigned)(dx0 + e) < (unsigned)K) P[dx0 + e] = acc[e];
+                }
+            };
+            auto tptr = [&](int task) {
+                const int r = task / nseg;
+                return tlev + ((size_t)(by0 + r) * g.nsx[L] + sa + task - r * nseg) * segsz + (size_t)lane * SG::LE;
+            };
+            if constexpr (CPT > 0 && PF) {
+                // the next task's target fragments load while this task's MFMAs run (two register sets,
+                // the loop unrolled by two so the sets alternate without copies)
+                auto tload = [&](frag (&t)[NLS], int task) {
+                    const T* tsb = tptr(task);
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                };
+                auto tmma = [&](const frag (&t)[NLS], int task) {
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) {
+                        f32x4 acc = {};
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ls += NP) {
+                            frag u[NP];
+                            qget(u, s, ls);
+                            seg_mma<T, X3>(acc, t + ls, u);
+                        }
+                        put(acc, s, task);
+                    }
+                };
+                frag t0[NLS], t1[NLS];
+                int task = w;
+                if (task < ntask) tload(t0, task);
+                while (task < ntask) {
+                    if (task + kWaves < ntask) tload(t1, task + kWaves);
+                    tmma(t0, task);
+                    task += kWaves;
+                    if (task >= ntask) break;
+                    if (task + kWaves < ntask) tload(t0, task + kWaves);
+                    tmma(t1, task);
+                    task += kWaves;
+                }
+            } else if constexpr (CPT > 0) {
+                for (int task = w; task < ntask; task += kWaves) {
+                    frag tc[NLS];
+                    const T* tsb = tptr(task);
+#pragma unroll
+                    for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) {
+                        f32x4 acc = {};
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ls += NP) {
+                            frag u[NP];
+                            qget(u, s, ls);
+                            seg_mma<T, X3>(acc, tc + ls, u);
+                        }
+                        put(acc, s, task);
+                    }
+                }
+            } else {
+                for (int task = w; task < ntask; task += kWaves) {
+                    const T* tsb = tptr(task);
+                    f32x4 acc[kQS];
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) acc[s] = f32x4{};
+                    for (int ls = 0; ls < nls * NP; ls += NP) {
+                        frag t[NP];
+#pragma unroll
+                        for (int p = 0; p < NP; ++p) t[p] = *reinterpret_cast<const frag*>(tsb + (size_t)(ls + p) * 64 * SG::LE);
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) {
+                            frag u[NP];
+#pragma unroll
+                            for (int p = 0; p < NP; ++p)
+                                u[p] = *reinterpret_cast<const frag*>(qsb[s] + ((size_t)(ls + p) * 64 + lane) * SG::LE);
+                            seg_mma<T, X3>(acc[s], t, u);
+                        }
+                    }
+#pragma unroll
+                    for (int s = 0; s < kQS; ++s) put(acc[s], s, task);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const int idx = tid + i * kLookThreads;
+                if (idx >= kQ * D) break;
+                const int q = idx % kQ, a = idx / kQ;
+                const float fx = sfx[L][q];
+                const float* P = S + q * KKp + a;
+#pragma unroll
+                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, P[jj * K + 1] - P[jj * K], P[jj * K]);
+            }
+            __syncthreads();                           // S is free for the next level
+        } else if (ntask > 0) {
+            // a box of more than kMaxTasks segments (flow differing by hundreds of pixels inside one
+            // block): each query's own (2r+2)^2 patch, one dot product per thread
+            for (int idx = tid; idx < kQ * KK; idx += kLookThreads) {
+                const int q = idx / KK, r = idx - q * KK;
+                const int ty = sys[L][q] + r / K, tx = sxs[L][q] + r % K;
+                float acc = 0.f;
+                if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
+                    const int qr = q / kBX, qc = q % kBX;
+                    const T* qs = qsb[qr * QSX + qc / 16];
+                    const T* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
+                    for (int c = 0; c < g.C; ++c)
+                        acc = fmaf(seg_elem<T, X3>(qs, qc % 16, c), seg_elem<T, X3>(ts, tx & 15, c), acc);
+                }
+                S[q * KKp + r] = acc;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const int idx = tid + i * kLookThreads;
+                if (idx >= kQ * D) break;
+                const int q = idx % kQ, a = idx / kQ;
+                const float fx = sfx[L][q];
+                const float* P = S + q * KKp + a;
+#pragma unroll
+                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, P[jj * K + 1] - P[jj * K], P[jj * K]);
+            }
+            __syncthreads();                           // S is free for the next level
+        }
+
+        // y-interpolation and the (a, b)-major output planes
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
             const int idx = tid + i * kLookThreads;
@@ -508,16 +533,11 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             const int q = idx % kQ, a = idx / kQ;
             const int y = qy0 + q / kBX, x = qx0 + q % kBX;
             if (y >= g.H || x >= g.W) continue;
-            const float fx = sfx[L][q];
-            const float fy = sfy[L][q] + (fx - fx);    // a NaN x weight reaches every row
-            const float* P = S + L * LP + q * KKp + a;
-            float hx[K];
-#pragma unroll
-            for (int jj = 0; jj < K; ++jj) hx[jj] = fmaf(fx, P[jj * K + 1] - P[jj * K], P[jj * K]);
+            const float fy = sfy[L][q] + (sfx[L][q] - sfx[L][q]);   // a NaN x weight reaches rows outside the band too
             if (RMD_OTF_ABL == 1 && fy != 12345.f) continue;
             float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
-            for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[bb + 1] - hx[bb], hx[bb]);
+            for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
         }
     }
 }
@@ -934,10 +954,10 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
         using QB = QBlock<QX, QY>;                                                                             \
-        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, QLK>;                                             \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK, QLK>;                                        \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
-        const size_t lds = sizeof(float) * levels * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +             \
+        const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +                      \
                            (QLK && CC > 0 ? (size_t)QB::kQS * 16 * CC * XN * sizeof(T) : 0);                    \
         RMD_REQUIRE(lds <= 160 * 1024, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: %zu B of LDS per block", lds);      \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -953,31 +973,33 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         case 256: RMD_OTF(T, RR, 256, QX, QY, OC); break;            \
         default: RMD_OTF(T, RR, 0, QX, QY, OC); break;               \
     }
-// radius 5-8: 16 x 1 query blocks (every level's patches of a larger block can exceed the 160-KB LDS)
 #define RMD_OTF_R(T, QX, QY, OC)                                     \
     switch (radius) {                                                \
         case 1: RMD_OTF_C(T, 1, QX, QY, OC); break;                  \
         case 2: RMD_OTF_C(T, 2, QX, QY, OC); break;                  \
         case 3: RMD_OTF_C(T, 3, QX, QY, OC); break;                  \
         case 4: RMD_OTF_C(T, 4, QX, QY, OC); break;                  \
-        case 5: RMD_OTF_C(T, 5, 1, 1, 1); break;                     \
-        case 6: RMD_OTF_C(T, 6, 1, 1, 1); break;                     \
-        case 7: RMD_OTF_C(T, 7, 1, 1, 1); break;                     \
-        default: RMD_OTF_C(T, 8, 1, 1, 1); break;                    \
+        case 5: RMD_OTF_C(T, 5, QX, QY, OC); break;                  \
+        case 6: RMD_OTF_C(T, 6, QX, QY, OC); break;                  \
+        case 7: RMD_OTF_C(T, 7, QX, QY, OC); break;                  \
+        default: RMD_OTF_C(T, 8, QX, QY, OC); break;                 \
     }
     if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
+        constexpr bool PFK = RMD_OTF_PF_B != 0;
         constexpr bool QLK = RMD_OTF_QL_B != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
+        constexpr bool PFK = RMD_OTF_PF_X != 0;
         constexpr bool QLK = RMD_OTF_QL_X != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
+        constexpr bool PFK = false;
         constexpr bool QLK = false;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
