@@ -40,11 +40,11 @@ constexpr int kThreads = 256;                        // prepare kernels
 #endif
 constexpr int kLookThreads = RMD_OTF_NT, kWaves = kLookThreads / 64;   // lookup workgroup
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
-// Query block and occupancy per compute (-D knobs for A/B builds, tools/_gpu_r03c.sh).  cfg2, one box
-// (profiles/otf_block_ab_r03.json): bf16 16x1 blocks at 2 workgroups per CU 90 us vs 16x2 at one 112 us
-// (16x4: 147, 32x1: 103 — larger boxes waste MFMA tiles and cut the number of blocks in flight; the
-// kernel is latency-bound at ~13 % of the MFMA rate it issues); split-bf16 16x2 at 2 per CU 203 vs
-// 214 us (16x1: 211).
+// Query block, occupancy and query-fragment placement per compute (-D knobs for A/B builds,
+// tools/_gpu_r03k.sh).  cfg2 bf16, one box per comparison (profiles/otf_patch_ab_r03.jsonl,
+// otf_ql_ab_r03.jsonl): 16x2 blocks with the query fragments in LDS (QL) 77.7 us; 16x1 with them in
+// registers 87.5; 16x4 in registers 84.8; 16x4 QL 100.7 at 256 threads, 77.2 at 512.  Split-bf16 keeps
+// 16x2 with register fragments (203 us; QL 303: three MFMAs per LDS fragment pair read).
 #ifndef RMD_OTF_QSX_B
 #define RMD_OTF_QSX_B 1
 #endif
@@ -63,21 +63,15 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_OCC_X
 #define RMD_OTF_OCC_X 2
 #endif
-#ifndef RMD_OTF_PF_B
-#define RMD_OTF_PF_B 0
-#endif
 #ifndef RMD_OTF_QL_B
 #define RMD_OTF_QL_B 1
 #endif
 #ifndef RMD_OTF_QL_X
 #define RMD_OTF_QL_X 0
 #endif
-// ablations for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks
+// ablation for A/B timing only (wrong results): 1 = no output stores
 #ifndef RMD_OTF_ABL
 #define RMD_OTF_ABL 0
-#endif
-#ifndef RMD_OTF_PF_X
-#define RMD_OTF_PF_X 0
 #endif
 #ifndef RMD_OTF_QSX_X
 #define RMD_OTF_QSX_X 1
@@ -263,7 +257,7 @@ template <int QSX, int QSY> struct QBlock {
 // run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool PF, bool QL>
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool QL>
 __global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
@@ -380,7 +374,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
 #pragma unroll
             for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
 
-        if (RMD_OTF_ABL != 2 && ntask > 0 && ntask <= kMaxTasks) {
+        if (ntask > 0 && ntask <= kMaxTasks) {
             // every query's (2r+2)^2 patch in LDS, zero where the target is off the map (zero padding)
             for (int i = tid; i < kQ * KKp; i += kLookThreads) S[i] = 0.f;
             // the lane's query in each query segment: its window origin at this level
@@ -409,40 +403,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 const int r = task / nseg;
                 return tlev + ((size_t)(by0 + r) * g.nsx[L] + sa + task - r * nseg) * segsz + (size_t)lane * SG::LE;
             };
-            if constexpr (CPT > 0 && PF) {
-                // the next task's target fragments load while this task's MFMAs run (two register sets,
-                // the loop unrolled by two so the sets alternate without copies)
-                auto tload = [&](frag (&t)[NLS], int task) {
-                    const T* tsb = tptr(task);
-#pragma unroll
-                    for (int ls = 0; ls < NLS; ++ls) t[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
-                };
-                auto tmma = [&](const frag (&t)[NLS], int task) {
-#pragma unroll
-                    for (int s = 0; s < kQS; ++s) {
-                        f32x4 acc = {};
-#pragma unroll
-                        for (int ls = 0; ls < NLS; ls += NP) {
-                            frag u[NP];
-                            qget(u, s, ls);
-                            seg_mma<T, X3>(acc, t + ls, u);
-                        }
-                        put(acc, s, task);
-                    }
-                };
-                frag t0[NLS], t1[NLS];
-                int task = w;
-                if (task < ntask) tload(t0, task);
-                while (task < ntask) {
-                    if (task + kWaves < ntask) tload(t1, task + kWaves);
-                    tmma(t0, task);
-                    task += kWaves;
-                    if (task >= ntask) break;
-                    if (task + kWaves < ntask) tload(t0, task + kWaves);
-                    tmma(t1, task);
-                    task += kWaves;
-                }
-            } else if constexpr (CPT > 0) {
+            if constexpr (CPT > 0) {
                 for (int task = w; task < ntask; task += kWaves) {
                     frag tc[NLS];
                     const T* tsb = tptr(task);
@@ -954,7 +915,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
         using QB = QBlock<QX, QY>;                                                                             \
-        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, PFK, QLK>;                                        \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, QLK>;                                             \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
         const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +                      \
@@ -987,19 +948,16 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
     if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
-        constexpr bool PFK = RMD_OTF_PF_B != 0;
         constexpr bool QLK = RMD_OTF_QL_B != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
-        constexpr bool PFK = RMD_OTF_PF_X != 0;
         constexpr bool QLK = RMD_OTF_QL_X != 0;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
-        constexpr bool PFK = false;
         constexpr bool QLK = false;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
