@@ -73,12 +73,6 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_ABL
 #define RMD_OTF_ABL 0
 #endif
-#ifndef RMD_OTF_QSX_X
-#define RMD_OTF_QSX_X 1
-#endif
-#ifndef RMD_OTF_QSY_X
-#define RMD_OTF_QSY_X 2
-#endif
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
