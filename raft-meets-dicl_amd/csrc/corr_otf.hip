@@ -35,10 +35,13 @@ namespace rmd {
 namespace {
 
 constexpr int kThreads = 256;                        // prepare kernels
-#ifndef RMD_OTF_NT
-#define RMD_OTF_NT 256
+// lookup workgroup size per compute (-D knobs)
+#ifndef RMD_OTF_NT_B
+#define RMD_OTF_NT_B 256
 #endif
-constexpr int kLookThreads = RMD_OTF_NT, kWaves = kLookThreads / 64;   // lookup workgroup
+#ifndef RMD_OTF_NT_X
+#define RMD_OTF_NT_X 256
+#endif
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block, occupancy and query-fragment placement per compute (-D knobs for A/B builds,
 // tools/_gpu_r03k.sh).  cfg2 bf16, one box per comparison (profiles/otf_patch_ab_r03.jsonl,
@@ -251,7 +254,7 @@ template <int QSX, int QSY> struct QBlock {
 // run on the same XCD and share its L2.  One block runs every level of its queries, so the query
 // staging, the coords load and the block's fixed start-up cost are paid once, not once per level.
 // CPT = compiled Cp (0: runtime multiple of 128).
-template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool QL>
+template <typename T, bool X3, int R, int CPT, int QSX, int QSY, int OCC, bool QL, int kLookThreads>
 __global__ void __launch_bounds__(kLookThreads, OCC)
 otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeom g,
                   const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
@@ -259,6 +262,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     using frag = typename SG::frag;
     using QB = QBlock<QSX, QSY>;
     constexpr int kQS = QB::kQS, kBX = QB::kBX, kBY = QB::kBY, kQ = QB::kQ;
+    constexpr int kWaves = kLookThreads / 64;
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = KK + 1;   // odd patch stride: queries spread over banks
     extern __shared__ float S[];                       // [kQ][KKp]: every query's (2r+2)^2 patch
     // every level's window origins / fractions and the block's bounding box per level, computed once
@@ -909,7 +913,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
 #define RMD_OTF(T, RR, CC, QX, QY, OC)                                                                         \
     do {                                                                                                       \
         using QB = QBlock<QX, QY>;                                                                             \
-        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, QLK>;                                             \
+        auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, QLK, NTK>;                                        \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
         const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +                      \
@@ -918,7 +922,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                   \
         const T* q = reinterpret_cast<const T*>(workspace);                                                    \
-        k<<<(unsigned)nblk, kLookThreads, lds, st>>>(q, q + qn * XN, g, coords, zero_level_mask, out);          \
+        k<<<(unsigned)nblk, NTK, lds, st>>>(q, q + qn * XN, g, coords, zero_level_mask, out);                   \
     } while (0)
 #define RMD_OTF_C(T, RR, QX, QY, OC)                                 \
     switch (cpt) {                                                   \
@@ -943,16 +947,19 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool QLK = RMD_OTF_QL_B != 0;
+        constexpr int NTK = RMD_OTF_NT_B;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_B, RMD_OTF_QSY_B, RMD_OTF_OCC_B)
     } else if (x3) {
         constexpr bool XS = true;
         constexpr size_t XN = 2;                    // query segments: qn split pairs
         constexpr bool QLK = RMD_OTF_QL_X != 0;
+        constexpr int NTK = RMD_OTF_NT_X;
         RMD_OTF_R(__bf16, RMD_OTF_QSX_X, RMD_OTF_QSY_X, RMD_OTF_OCC_X)
     } else {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool QLK = false;
+        constexpr int NTK = RMD_OTF_NT_X;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
 #undef RMD_OTF_R
