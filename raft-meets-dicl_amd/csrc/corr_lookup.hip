@@ -99,6 +99,12 @@ __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, in
 // per-image level slab is below 2^31 bytes.
 constexpr unsigned kOOB = 0x80000000u;
 
+// A/B ablation builds only (tools/build_variant.sh): bit 0 drops the output stores, bit 1 the pyramid
+// loads, by sending them to kOOB (same instruction stream, no memory traffic).  0 in the product.
+#ifndef RMD_LOOKUP_ABL
+#define RMD_LOOKUP_ABL 0
+#endif
+
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const PyrGeom& g, int L, int b) {
     const long long per = (long long)g.ty[L] * g.tx[L] * g.slots * g.th[L] * g.tw[L];     // elements per image
@@ -112,6 +118,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const
 
 template <int NW>
 __device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_rsrc_t rs, unsigned off) {
+    if constexpr ((RMD_LOOKUP_ABL & 2) != 0) off = kOOB;
     if constexpr (NW == 4) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
 #pragma unroll
@@ -174,7 +181,7 @@ __device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, b
     OutBuf r;
     r.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
                                              (int)((unsigned)D * D * N * 4u), 0x00020000);
-    r.voff = active ? (unsigned)p * 4u : kOOB;
+    r.voff = (active && (RMD_LOOKUP_ABL & 1) == 0) ? (unsigned)p * 4u : kOOB;
     return r;
 }
 

@@ -64,9 +64,14 @@ def corr_options(parameters=None, **overrides):
     as the reference's from_config does for bad types."""
     base = _current
     p = dict(parameters or {})
-    precision = overrides.get("precision") or p.get("corr-precision", base.precision)
-    method = overrides.get("method") or p.get("corr-method", base.method)
-    budget = overrides.get("memory_budget") or p.get("corr-memory-budget", base.memory_budget)
+    def pick(key, pkey, default):
+        # an explicit override wins even when falsy (0, ''): it then reaches the validation below
+        v = overrides.get(key)
+        return v if v is not None else p.get(pkey, default)
+
+    precision = pick("precision", "corr-precision", base.precision)
+    method = pick("method", "corr-method", base.method)
+    budget = pick("memory_budget", "corr-memory-budget", base.memory_budget)
     if precision not in PRECISIONS:
         raise ValueError(f"unknown corr-precision '{precision}', expected one of {list(PRECISIONS)}")
     if method not in METHODS:
@@ -106,9 +111,19 @@ def volume_bytes(batch, height, width, levels, precision, training):
     return b
 
 
-def choose_method(method, batch, height, width, levels, precision, training, budget):
+OTF_BACKWARD_MAX_CHANNELS = 256       # rmd_corr_otf_backward's limit (include/rmd.h)
+
+
+def choose_method(method, batch, height, width, levels, precision, training, budget, channels=None):
     """'volume' or 'otf' for a block: explicit methods pass through; 'auto' takes the volume while it
-    fits the budget."""
+    fits the budget.  A training block with more than 256 channels has no on-the-fly backward: 'auto'
+    keeps the volume for it and an explicit 'otf' raises here, at construction, instead of in backward."""
+    otf_trainable = not training or channels is None or channels <= OTF_BACKWARD_MAX_CHANNELS
+    if method == "otf" and not otf_trainable:
+        raise ValueError(f"corr-method 'otf' cannot train a block with {channels} channels "
+                         f"(the on-the-fly backward supports C <= {OTF_BACKWARD_MAX_CHANNELS}); use 'volume'")
     if method != "auto":
         return method
+    if not otf_trainable:
+        return "volume"
     return "otf" if volume_bytes(batch, height, width, levels, precision, training) > budget else "volume"

@@ -7,7 +7,7 @@ and, where the reference's module is trained through it, an autograd formula who
 an rmd operator.  Schemas follow SURVEY.md §8(b):
 
   corr_pyramid(fmap1, fmap2, levels, compute, storage, scale) -> pyramid     raft.py:18-47
-  corr_lookup(pyramid, coords, levels, radius, level_mask, layout) -> corr   raft.py:49-95
+  corr_lookup(pyramid, coords, levels, radius, level_mask) -> corr           raft.py:49-95
   corr_otf_prepare / corr_otf_lookup                                        raft_fs.py:13-87, corr/dot.py:25-57
   dicl_stack(fmap1, fmap2, coords, radius, level, norm_h, norm_w, extra) ->  corr/dicl.py:26-54,
         (B, 2r+1, 2r+1, 2C[+2], h, w)                                        dicl_emb.py:51-89, raft_dicl_ml.py:294-315
@@ -35,8 +35,7 @@ LIB = torch.library.Library("rmd", "DEF")
 
 _SCHEMAS = {
     "corr_pyramid": "corr_pyramid(Tensor fmap1, Tensor fmap2, int levels, int compute, int storage, float scale) -> Tensor",
-    "corr_lookup": ("corr_lookup(Tensor pyramid, Tensor coords, int levels, int radius, int level_mask, int layout) "
-                    "-> Tensor"),
+    "corr_lookup": "corr_lookup(Tensor pyramid, Tensor coords, int levels, int radius, int level_mask) -> Tensor",
     "corr_otf_prepare": "corr_otf_prepare(Tensor fmap1, Tensor fmap2, int levels, int compute, float scale) -> Tensor",
     "corr_otf_lookup": ("corr_otf_lookup(Tensor workspace, Tensor coords, int channels, int levels, int compute, "
                         "int radius, int level_mask) -> Tensor"),
@@ -131,6 +130,26 @@ def describe_for(batch, height, width, levels, storage, channels, compute):
 _STORAGE = {_lib.RMD_F32: torch.float32, _lib.RMD_F16: torch.float16}
 _STORAGE_CODE = {torch.float32: _lib.RMD_F32, torch.float16: _lib.RMD_F16}
 
+# The pyramid tensor carries its layout in its shape, so corr_lookup never trusts a caller's word for
+# it: RMD_LAYOUT_ROWS pyramids are 1-D (total_elements,), RMD_LAYOUT_TILES pyramids 2-D
+# (total_elements / 8, 8) — one row per 2 x 4 chunk (every tiles level holds a multiple of 64 elements).
+TILES_ROW = 8
+
+
+def pyramid_view(data, layout):
+    """The flat pyramid allocation shaped for its layout (see TILES_ROW)."""
+    return data.view(-1, TILES_ROW) if layout == _lib.RMD_LAYOUT_TILES else data
+
+
+def pyramid_layout(pyramid):
+    """Layout of a pyramid tensor from its shape; ValueError for any other shape."""
+    if pyramid.dim() == 1:
+        return _lib.RMD_LAYOUT_ROWS
+    if pyramid.dim() == 2 and pyramid.shape[1] == TILES_ROW:
+        return _lib.RMD_LAYOUT_TILES
+    raise ValueError(f"corr_lookup: a pyramid is 1-D (row layout) or (n, {TILES_ROW}) (tiles layout), "
+                     f"got shape {tuple(pyramid.shape)}")
+
 
 # ---- RAFT correlation pyramid + lookup (inference operators) -----------------------------------
 
@@ -152,14 +171,15 @@ def _corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
     with _Dev(f1) as st:
         _lib.check(lib.rmd_corr_pyramid(_ptr(f1), _ptr(f2), c, float(scale), ctypes.byref(d), compute, _ptr(data),
                                         _ptr(ws), st), "rmd_corr_pyramid")
-    return data
+    return pyramid_view(data, d.layout)
 
 
 @_fake("corr_pyramid")
 def _(fmap1, fmap2, levels, compute, storage, scale):
     _check_fmaps(fmap1, fmap2)
     b, c, h, w = fmap1.shape
-    return fmap1.new_empty((describe_for(b, h, w, levels, storage, c, compute).total_elements,), dtype=_STORAGE[storage])
+    d = describe_for(b, h, w, levels, storage, c, compute)
+    return pyramid_view(fmap1.new_empty((d.total_elements,), dtype=_STORAGE[storage]), d.layout)
 
 
 def _lookup_out(pyramid, coords, levels, radius):
@@ -175,11 +195,12 @@ def _check_device(name, *ts):
 
 
 @_cuda("corr_lookup")
-def _corr_lookup(pyramid, coords, levels, radius, level_mask, layout):
+def _corr_lookup(pyramid, coords, levels, radius, level_mask):
     b, two, h, w = coords.shape
-    if pyramid.dtype not in _STORAGE_CODE or pyramid.dim() != 1 or not pyramid.is_contiguous():
-        raise ValueError(f"corr_lookup: pyramid must be a contiguous 1-D float32/float16 tensor, got "
+    if pyramid.dtype not in _STORAGE_CODE or not pyramid.is_contiguous():
+        raise ValueError(f"corr_lookup: pyramid must be a contiguous float32/float16 tensor, got "
                          f"{pyramid.dtype} {tuple(pyramid.shape)}")
+    layout = pyramid_layout(pyramid)
     _check_device("corr_lookup", pyramid, coords)
     d = describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype], layout)
     if two != 2 or pyramid.numel() != d.total_elements:
@@ -193,7 +214,8 @@ def _corr_lookup(pyramid, coords, levels, radius, level_mask, layout):
 
 
 @_fake("corr_lookup")
-def _(pyramid, coords, levels, radius, level_mask, layout):
+def _(pyramid, coords, levels, radius, level_mask):
+    pyramid_layout(pyramid)
     return _lookup_out(pyramid, coords, levels, radius)
 
 

@@ -46,7 +46,8 @@ _STORAGE_DTYPE = {RMD_F32: torch.float32, RMD_F16: torch.float16}
 
 
 class Pyramid:
-    """Correlation pyramid in the tiled, query-minor HBM layout of include/rmd.h."""
+    """Correlation pyramid in the tiled, query-minor HBM layout of include/rmd.h.  ``data`` is 1-D in the
+    row layout and (n, 8) in the tiles layout (rmd.library.pyramid_view)."""
 
     def __init__(self, data, desc, channels, scale):
         self.data = data
@@ -69,7 +70,7 @@ class Pyramid:
         hl, wl = d.level_h[i], d.level_w[i]
         s = d.query_slots
         off = d.level_offset[i]
-        x = self.data[off: off + b * ty * tx * s * th * tw].view(b, ty, tx, s, th, tw)
+        x = self.data.reshape(-1)[off: off + b * ty * tx * s * th * tw].view(b, ty, tx, s, th, tw)
         x = x.permute(0, 3, 1, 4, 2, 5).reshape(b, s, ty * th, tx * tw)[..., :hl, :wl]
         if d.layout == _lib.RMD_LAYOUT_TILES:
             x = x.index_select(1, torch.as_tensor(tiles_slots(h, w), device=x.device))
@@ -108,7 +109,8 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     lib = _lib.lib()
     ws = torch.empty(lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), c, compute), dtype=torch.uint8,
                      device=f1.device)
-    data = torch.empty(d.total_elements, dtype=_STORAGE_DTYPE[storage], device=f1.device)
+    data = library.pyramid_view(torch.empty(d.total_elements, dtype=_STORAGE_DTYPE[storage], device=f1.device),
+                                d.layout)
     with torch.cuda.device(f1.device):
         stream = _lib.stream_ptr(f1.device)
         _lib.check(lib.rmd_corr_prepare(_ptr(f1), _ptr(f2), c, scale, ctypes.byref(d), compute, _ptr(ws), stream),
@@ -128,7 +130,7 @@ def corr_lookup(pyr, coords, radius, mask_costs=()):
     d = pyr.desc
     if tuple(coords.shape) != (d.batch, 2, d.height, d.width):
         raise ValueError(f"coords must be (B,2,H,W)=({d.batch},2,{d.height},{d.width}), got {tuple(coords.shape)}")
-    return torch.ops.rmd.corr_lookup(pyr.data, coords, d.levels, radius, _mask_bits(mask_costs, d.levels), d.layout)
+    return torch.ops.rmd.corr_lookup(pyr.data, coords, d.levels, radius, _mask_bits(mask_costs, d.levels))
 
 
 # ---- on-the-fly lookup (raft_fs semantics without the volume) -------------------------------------

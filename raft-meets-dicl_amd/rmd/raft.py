@@ -37,7 +37,7 @@ class CorrBlock:
         training = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
         b, c, h, w = fmap1.shape
         self.method = config.choose_method(opts.method, b, h, w, num_levels, self.precision, training,
-                                           opts.memory_budget)
+                                           opts.memory_budget, channels=c)
         scale = float(c) ** -0.5 if self.scale is None else float(self.scale)
         if self.method == "otf":
             self.pyramid = None

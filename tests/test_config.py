@@ -1,0 +1,62 @@
+"""Host logic of rmd.config (op selection from cfg/model ``parameters``; SURVEY.md §5 "Config / flags")."""
+
+import pytest
+
+from rmd import config
+
+
+def test_defaults_reproduce_the_reference():
+    o = config.corr_options({})
+    assert o.precision == config.current().precision
+    assert o.method == config.current().method
+
+
+def test_parameters_and_overrides():
+    o = config.corr_options({"corr-precision": "bf16", "corr-method": "volume", "corr-memory-budget": "2GiB"})
+    assert o == ("bf16", "volume", 2 << 30)
+    o = config.corr_options({"corr-precision": "bf16"}, precision="fp32-exact", memory_budget=4096)
+    assert o.precision == "fp32-exact" and o.memory_budget == 4096
+    assert config.corr_options(None, **o.kwargs()) == o
+    assert config.corr_options(o.parameters()) == o
+
+
+@pytest.mark.parametrize("kw", [{"memory_budget": 0}, {"memory_budget": -5}, {"precision": ""}, {"method": ""},
+                                {"precision": "fp64"}, {"method": "fast"}])
+def test_explicit_invalid_overrides_raise(kw):
+    # falsy explicit values reach the validation instead of silently falling back
+    with pytest.raises(ValueError):
+        config.corr_options({}, **kw)
+
+
+def test_budget_strings():
+    assert config._bytes("64KiB") == 64 << 10
+    assert config._bytes("1.5 GiB") == 3 << 29
+    with pytest.raises(ValueError):
+        config._bytes("lots")
+
+
+def test_auto_method_by_budget():
+    small = config.choose_method("auto", 1, 8, 8, 4, "bf16", False, 1 << 30)
+    big = config.choose_method("auto", 8, 270, 480, 4, "bf16", False, 1 << 30)
+    assert (small, big) == ("volume", "otf")
+    assert config.choose_method("volume", 8, 270, 480, 4, "bf16", False, 1) == "volume"
+
+
+def test_otf_training_channel_limit():
+    # the on-the-fly backward takes C <= 256: auto keeps the volume for wider training blocks and an
+    # explicit 'otf' fails at construction, not in backward
+    assert config.choose_method("auto", 8, 270, 480, 4, "bf16", True, 1 << 30, channels=256) == "otf"
+    assert config.choose_method("auto", 8, 270, 480, 4, "bf16", True, 1 << 30, channels=320) == "volume"
+    assert config.choose_method("auto", 8, 270, 480, 4, "bf16", False, 1 << 30, channels=320) == "otf"
+    with pytest.raises(ValueError, match="C <= 256"):
+        config.choose_method("otf", 8, 270, 480, 4, "bf16", True, 1 << 30, channels=512)
+    assert config.choose_method("otf", 8, 270, 480, 4, "bf16", False, 1 << 30, channels=512) == "otf"
+
+
+def test_configure_restore():
+    prev = config.configure({"corr-precision": "bf16"})
+    try:
+        assert config.current().precision == "bf16"
+    finally:
+        config.restore(prev)
+    assert config.current() == prev

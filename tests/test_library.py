@@ -31,8 +31,14 @@ def test_fake_kernels_propagate_shapes():
         pyr = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16, _lib.RMD_F16, 0.0625)
         d = _lib.describe(2, 55, 128, 4, _lib.RMD_F16, _lib.RMD_LAYOUT_TILES)     # the w8 GEMM's layout
         assert pyr.dtype == torch.float16 and pyr.numel() == d.total_elements
+        assert pyr.shape == (d.total_elements // 8, 8)                              # tiles: (n, 8)
         co = torch.empty(2, 2, 55, 128, device="cuda")
-        assert torch.ops.rmd.corr_lookup(pyr, co, 4, 4, 0, d.layout).shape == (2, 324, 55, 128)
+        assert torch.ops.rmd.corr_lookup(pyr, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        rows = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16X3, _lib.RMD_F32, 0.0625)
+        assert rows.dim() == 1                                                       # row layout: 1-D
+        assert torch.ops.rmd.corr_lookup(rows, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        with pytest.raises(ValueError, match="tiles layout"):
+            torch.ops.rmd.corr_lookup(pyr.view(-1, 16), co, 4, 4, 0)
         f = torch.empty(2, 32, 12, 16, device="cuda")
         c2 = torch.empty(2, 2, 12, 16, device="cuda")
         assert torch.ops.rmd.dicl_stack(f, f, c2, 4, 0, 12, 16, False).shape == (2, 9, 9, 64, 12, 16)

@@ -3,7 +3,7 @@
 coordinates for the bf16 (tiles layout) and fp32 (row layout) pyramids, HIP events around each of 12
 lookups x reps; run once per library build (RMD_LIBRARY=...) on one box for an A/B.  Prints one JSON
 line with a checksum of one output (equal across builds = same results).
-usage: python3 tools/lookup_time.py [reps]"""
+usage: python3 tools/lookup_time.py [reps] [precision ...]"""
 import json
 import os
 import sys
@@ -19,9 +19,10 @@ from rmd import ops  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    precs = sys.argv[2:] or ["bf16", "fp32"]
     f1, f2, coords = bench.synthetic(8, 256, 55, 128, 12, 1234, "cuda")
     res = {"lib": os.path.basename(os.environ.get("RMD_LIBRARY", "librmd.so"))}
-    for p in ("bf16", "fp32"):
+    for p in precs:
         pyr = ops.corr_pyramid(f1, f2, 4, p)
         for i in range(12):
             ops.corr_lookup(pyr, coords[i], 4)
