@@ -1,7 +1,9 @@
 """rmd — MI355X-native (gfx950) cost-volume backend for qzed/raft-meets-dicl.
 
-Drop-in host mirror of the reference's hot-path modules; every compute call goes through the C ABI
-of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
+Drop-in host mirror of the reference's hot-path modules; every compute call on GPU tensors goes
+through the C ABI of librmd.so (include/rmd.h) on the current HIP stream and raises if the library
+is missing.  CPU tensors dispatch to the operators' CPU kernels (rmd/cpu.py: the reference's ATen
+algorithm), so the modules also run on device='cpu' as the reference's do.
 
   rmd.raft.CorrBlock                    <- src/models/impls/raft.py:15-95
   rmd.raft_fs.CorrBlock                 <- src/models/impls/raft_fs.py:13-87
@@ -14,7 +16,7 @@ of librmd.so (include/rmd.h) on the current HIP stream.  No CPU fallback.
   rmd.input.InputSpec / ModuloPadding   <- src/models/input.py:32-313 (frame pair + flow target format)
 """
 
-from . import blocks, config, corr, dicl, heads, input, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
+from . import blocks, config, corr, cpu, dicl, heads, input, ops, raft, raft_dicl_ml, raft_fs, warp  # noqa: F401
 from .ops import set_default_precision, get_default_precision  # noqa: F401
 
 __version__ = "0.1"

@@ -2,9 +2,10 @@
 
 Every operator has a CUDA (HIP) kernel — the ctypes call into include/rmd.h on torch's current
 stream —, a fake (meta) implementation that only computes output shapes (torch.compile /
-torch.export / FakeTensor tracing), an explicit CPU kernel that raises (there is no CPU fallback),
-and, where the reference's module is trained through it, an autograd formula whose backward is again
-an rmd operator.  Schemas follow SURVEY.md §8(b):
+torch.export / FakeTensor tracing), a CPU kernel for CPU tensors (rmd/cpu.py: the reference's ATen
+algorithm, registered for CPU and AutogradCPU — a dispatch by device, never a fallback for a GPU
+tensor), and, where the reference's module is trained through it, an autograd formula whose backward
+is again an rmd operator.  Schemas follow SURVEY.md §8(b):
 
   corr_pyramid(fmap1, fmap2, levels, compute, storage, scale) -> pyramid     raft.py:18-47
   corr_lookup(pyramid, coords, levels, radius, level_mask) -> corr           raft.py:49-95
@@ -63,14 +64,16 @@ for _s in _SCHEMAS.values():
     LIB.define(_s)
 
 
-def _no_cpu(*args, **kwargs):
-    raise RuntimeError("rmd: HIP kernels need GPU tensors (no CPU fallback exists)")
-
-
 def _cuda(name):
+    """The HIP kernel of an operator (CUDA dispatch key); its CPU kernel lives in rmd/cpu.py.  Every
+    tensor argument must be a GPU tensor (the dispatcher picks this kernel when any one is)."""
     def deco(fn):
-        LIB.impl(name, fn, "CUDA")
-        LIB.impl(name, _no_cpu, "CPU")
+        def kernel(*args):
+            for a in args:
+                if isinstance(a, torch.Tensor) and a.device.type != "cuda":
+                    raise ValueError(f"rmd::{name}: all tensors must be on the GPU, got one on {a.device}")
+            return fn(*args)
+        LIB.impl(name, kernel, "CUDA")
         return fn
     return deco
 
@@ -178,7 +181,10 @@ def _corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
 def _(fmap1, fmap2, levels, compute, storage, scale):
     _check_fmaps(fmap1, fmap2)
     b, c, h, w = fmap1.shape
-    d = describe_for(b, h, w, levels, storage, c, compute)
+    if fmap1.device.type == "cpu":                  # rmd/cpu.py writes the row layout
+        d = describe(b, h, w, levels, storage)
+    else:
+        d = describe_for(b, h, w, levels, storage, c, compute)
     return pyramid_view(fmap1.new_empty((d.total_elements,), dtype=_STORAGE[storage]), d.layout)
 
 
@@ -238,6 +244,9 @@ def _corr_otf_prepare(fmap1, fmap2, levels, compute, scale):
 @_fake("corr_otf_prepare")
 def _(fmap1, fmap2, levels, compute, scale):
     b, c, h, w = fmap1.shape
+    if fmap1.device.type == "cpu":                  # rmd/cpu.py: fmap1 * scale + pooled levels, float32
+        n = b * c * (h * w + sum((h >> i) * (w >> i) for i in range(levels)))
+        return fmap1.new_empty((n,), dtype=torch.float32)
     return fmap1.new_empty((_lib.lib().rmd_corr_otf_workspace_bytes(b, c, h, w, levels, compute),), dtype=torch.uint8)
 
 

@@ -1,7 +1,10 @@
 """Torch-facing wrappers over the C ABI (include/rmd.h): device checks, allocation, streams.
 
 Outputs and workspaces come from torch's caching allocator; the C launchers only enqueue kernels
-on torch's current HIP stream.  Every function requires GPU tensors and raises otherwise.
+on torch's current HIP stream.  GPU tensors run the HIP kernels (and raise if librmd.so is missing);
+CPU tensors dispatch to the operators' CPU kernels (rmd/cpu.py, the reference's ATen algorithm).
+The token-linked autograd functions of the RAFT correlation and of the on-the-fly lookup are
+GPU-only: on the CPU the operators' own ATen graph carries the gradient.
 """
 
 import ctypes
@@ -35,7 +38,19 @@ def get_default_precision():
 def _require_gpu(*tensors):
     for t in tensors:
         if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
-            raise RuntimeError("rmd: HIP kernels need GPU tensors (no CPU fallback exists)")
+            raise RuntimeError("rmd: HIP kernels need GPU tensors")
+
+
+def _same_device(*tensors):
+    """All inputs on one device: GPU tensors run the HIP kernels, CPU tensors the CPU kernels."""
+    dev = None
+    for t in tensors:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"rmd: expected a tensor, got {type(t).__name__}")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"rmd: tensors on different devices ({dev} / {t.device})")
 
 
 def _ptr(t):
@@ -95,15 +110,17 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     (the operand prep runs before the start event) — bench.py's roofline timing; that call runs the
     same two C-ABI halves (rmd_corr_prepare, rmd_corr_pyramid_prepared) directly.
     """
-    _require_gpu(fmap1, fmap2)
+    _same_device(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
     compute, storage = PRECISIONS[precision or get_default_precision()]
     b, c, h, w = fmap1.shape
     scale = 1.0 / float(c) ** 0.5 if scale is None else float(scale)
-    d = library.describe_for(b, h, w, levels, storage, c, compute)
     if events is None:
-        return Pyramid(torch.ops.rmd.corr_pyramid(fmap1, fmap2, levels, compute, storage, scale), d, c, scale)
+        data = torch.ops.rmd.corr_pyramid(fmap1, fmap2, levels, compute, storage, scale)
+        return Pyramid(data, library.describe(b, h, w, levels, storage, library.pyramid_layout(data)), c, scale)
+    _require_gpu(fmap1, fmap2)
+    d = library.describe_for(b, h, w, levels, storage, c, compute)
     f1 = fmap1.detach().float().contiguous()
     f2 = fmap2.detach().float().contiguous()
     lib = _lib.lib()
@@ -125,8 +142,8 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
 
 
 def corr_lookup(pyr, coords, radius, mask_costs=()):
-    """raft.CorrBlock.__call__ (raft.py:49-95) on the GPU -> (B, L*(2r+1)^2, H, W) float32."""
-    _require_gpu(pyr.data, coords)
+    """raft.CorrBlock.__call__ (raft.py:49-95) -> (B, L*(2r+1)^2, H, W) float32."""
+    _same_device(pyr.data, coords)
     d = pyr.desc
     if tuple(coords.shape) != (d.batch, 2, d.height, d.width):
         raise ValueError(f"coords must be (B,2,H,W)=({d.batch},2,{d.height},{d.width}), got {tuple(coords.shape)}")
@@ -143,7 +160,7 @@ class OtfState:
 
 
 def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
-    _require_gpu(fmap1, fmap2)
+    _same_device(fmap1, fmap2)
     if fmap1.shape != fmap2.shape or fmap1.dim() != 4:
         raise ValueError(f"fmap1/fmap2 must be equal (B,C,H,W) shapes, got {tuple(fmap1.shape)} / {tuple(fmap2.shape)}")
     compute = PRECISIONS[precision or get_default_precision()][0]     # fp32: split bf16, fp32-exact: f32
@@ -153,7 +170,7 @@ def otf_prepare(fmap1, fmap2, levels, precision=None, scale=1.0):
 
 
 def otf_lookup(st, coords, radius, mask_costs=()):
-    _require_gpu(st.ws, coords)
+    _same_device(st.ws, coords)
     if tuple(coords.shape) != (st.b, 2, st.h, st.w):
         raise ValueError(f"coords must be (B,2,H,W)=({st.b},2,{st.h},{st.w}), got {tuple(coords.shape)}")
     return torch.ops.rmd.corr_otf_lookup(st.ws, coords, st.c, st.levels, st.compute, radius,
@@ -379,7 +396,7 @@ def _stream(t):
 def dicl_stack(fmap1, fmap2, coords, radius, level=0, norm_hw=None, extra_delta=False):
     """(B,C,h,w), (B,C,hl,wl), (B,2,h,w) -> (B, 2r+1, 2r+1, 2C[+2], h, w) MatchingNet input
     (torch.ops.rmd.dicl_stack; corr/dicl.py:26-54)."""
-    _require_gpu(fmap1, fmap2, coords)
+    _same_device(fmap1, fmap2, coords)
     nh, nw = norm_hw if norm_hw is not None else fmap1.shape[-2:]
     return torch.ops.rmd.dicl_stack(fmap1, fmap2, coords, radius, level, int(nh), int(nw), bool(extra_delta))
 
@@ -387,33 +404,33 @@ def dicl_stack(fmap1, fmap2, coords, radius, level=0, norm_hw=None, extra_delta=
 def dicl_stack_int(fmap1, fmap2, ru, rv):
     """Integer-displacement matching volume with occlusion mask (torch.ops.rmd.dicl_stack_int;
     impls/dicl.py:212-238)."""
-    _require_gpu(fmap1, fmap2)
+    _same_device(fmap1, fmap2)
     return torch.ops.rmd.dicl_stack_int(fmap1, fmap2, ru, rv)
 
 
 def dicl_stack_int_warped(fmap1, fmap2, flow, ru, rv):
     """Masked integer volume of (fmap1, warp_backwards(fmap2, flow)) in one fused pass pair
     (torch.ops.rmd.dicl_stack_int_warped; impls/dicl.py:178-181 + 212-238)."""
-    _require_gpu(fmap1, fmap2, flow)
+    _same_device(fmap1, fmap2, flow)
     return torch.ops.rmd.dicl_stack_int_warped(fmap1, fmap2, flow, ru, rv)
 
 
 def dap(x, weight):
     """x (B, D, ...) -> W x over the displacement dim; weight (D, D[, 1, 1]) (torch.ops.rmd.dap;
     blocks/dicl.py:143-150)."""
-    _require_gpu(x, weight)
+    _same_device(x, weight)
     return torch.ops.rmd.dap(x, weight)
 
 
 def up8(mask, flow, temperature=4.0):
     """mask (B, 576, h, w) logits, flow (B, 2, h, w) -> convex-upsampled flow (B, 2, 8h, 8w)
     (torch.ops.rmd.up8; raft.py:319-331)."""
-    _require_gpu(mask, flow)
+    _same_device(mask, flow)
     return torch.ops.rmd.up8(mask, flow, float(temperature))
 
 
 def softargmax(cost, levels, radius, temperature=1.0):
     """cost (B, >= L*(2r+1)^2, h, w) -> list of L flows (B, 2, h, w), level l scaled by 2^l
     (torch.ops.rmd.softargmax; raft.py:112-135, corr/dot.py:83-90)."""
-    _require_gpu(cost)
+    _same_device(cost)
     return list(torch.ops.rmd.softargmax(cost, levels, radius, float(temperature)).unbind(0))

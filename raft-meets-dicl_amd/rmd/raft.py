@@ -35,18 +35,21 @@ class CorrBlock:
         self.precision = opts.precision
         self._state = self._token = None
         training = torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad)
+        # GPU training runs the token-linked autograd functions of rmd.ops; on the CPU the operators'
+        # ATen kernels (rmd/cpu.py) carry the gradient themselves
+        tokens = training and fmap1.is_cuda
         b, c, h, w = fmap1.shape
         self.method = config.choose_method(opts.method, b, h, w, num_levels, self.precision, training,
                                            opts.memory_budget, channels=c)
         scale = float(c) ** -0.5 if self.scale is None else float(self.scale)
         if self.method == "otf":
             self.pyramid = None
-            if training:
+            if tokens:
                 self._otf, self._state, self._token = ops.otf_block_autograd(fmap1, fmap2, num_levels, self.precision,
                                                                              scale)
             else:
                 self._otf = ops.otf_prepare(fmap1, fmap2, num_levels, self.precision, scale=scale)
-        elif training:
+        elif tokens:
             self.pyramid, self._state, self._token = ops.corr_block_autograd(fmap1, fmap2, num_levels,
                                                                              self.precision, self.scale)
         else:

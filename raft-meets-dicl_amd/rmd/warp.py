@@ -9,11 +9,11 @@ img2 only (the reference's callers detach the flow, impls/dicl.py:178).
 
 import torch
 
-from .ops import _require_gpu
+from .ops import _same_device
 
 
 def warp_backwards(img2, flow, eps=1e-5):
     """warp img2 back to img1 based on flow -> (est1 * mask, mask) (torch.ops.rmd.warp_backwards)."""
-    _require_gpu(img2, flow)
+    _same_device(img2, flow)
     out, mask = torch.ops.rmd.warp_backwards(img2, flow, float(eps))
     return out.to(img2.dtype), mask.expand(img2.shape)

@@ -90,9 +90,35 @@ def test_describe_rejects_bad_shapes(args):
         _lib.describe(*args)
 
 
-def test_no_cpu_fallback():
+def test_gpu_path_fails_loudly_without_the_library(monkeypatch):
+    """No fallback: with librmd.so missing, the HIP path raises instead of computing anything else."""
+    from rmd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", "/nonexistent/librmd.so")
+    with pytest.raises(_lib.RmdError, match="HIP library not found"):
+        _lib.lib()
+
+
+def test_cpu_dispatch_launches_no_hip_kernel(monkeypatch):
+    """CPU tensors run the ATen kernels of rmd/cpu.py: the only C-ABI calls they make are the host-only
+    geometry helpers (no kernel launcher is ever reached), so the CPU path is a dispatch by device, not
+    a stand-in for the HIP path."""
     import torch
     import rmd
-    f = torch.zeros(1, 8, 8, 8)
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        rmd.raft.CorrBlock(f, f)
+    from rmd import _lib
+    real = _lib.lib()
+    allowed = {"rmd_pyramid_describe_layout", "rmd_pyramid_describe_for", "rmd_last_error"}
+
+    class HostOnly:
+        def __getattr__(self, name):
+            if name not in allowed:
+                raise AssertionError(f"CPU path reached {name}")
+            return getattr(real, name)
+
+    monkeypatch.setattr(_lib, "_lib", HostOnly())
+    f = torch.randn(1, 8, 8, 12)
+    co = torch.rand(1, 2, 8, 12) * 8
+    assert rmd.raft.CorrBlock(f, f, 2, 2, method="volume")(co).shape == (1, 50, 8, 12)
+    assert rmd.raft_fs.CorrBlock(f, f, 2, 2, method="otf")(co).shape == (1, 50, 8, 12)
+    assert rmd.ops.dicl_stack(f, f, co, 2).shape == (1, 5, 5, 16, 8, 12)
+    assert rmd.ops.dicl_stack_int(f, f, 1, 1).shape == (1, 3, 3, 16, 8, 12)

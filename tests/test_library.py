@@ -51,11 +51,16 @@ def test_fake_kernels_propagate_shapes():
         assert out.shape == f.shape and mask.shape == (2, 1, 12, 16) and mask.dtype == torch.bool
 
 
-def test_cpu_tensors_raise():
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        torch.ops.rmd.dap(torch.zeros(1, 81, 4), torch.zeros(81, 81))
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        torch.ops.rmd.dicl_stack_int(torch.zeros(1, 8, 4, 4), torch.zeros(1, 8, 4, 4), 1, 1)
+def test_cpu_tensors_dispatch_to_the_cpu_kernels():
+    """CPU tensors reach rmd/cpu.py (the reference's ATen algorithm; tests/test_cpu_dispatch.py checks
+    it against the golden vectors); mixed devices are rejected before any kernel runs."""
+    import torch.nn.functional as F
+    x, w = torch.randn(2, 81, 4, 5), torch.randn(81, 81)
+    assert torch.allclose(torch.ops.rmd.dap(x, w), F.conv2d(x, w[:, :, None, None]), atol=1e-5)
+    assert torch.ops.rmd.dicl_stack_int(torch.ones(1, 8, 4, 4), torch.ones(1, 8, 4, 4), 1, 1).shape == (1, 3, 3, 16, 4, 4)
+    from rmd import ops
+    with pytest.raises(ValueError, match="different devices"):
+        ops.dap(x, w.to("meta"))
 
 
 @pytest.mark.gpu
