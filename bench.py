@@ -66,8 +66,8 @@ def parse():
                          "pyramid) on the same inputs, with its own rooflines")
     ap.add_argument("--fp32-steps", type=int, default=10)
     ap.add_argument("--live-pmc", choices=["on", "off"], default="on",
-                    help="rank 0 of single-GPU runs: roofline traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes "
-                         "over tools/pmc_probe.py run as child processes in this run")
+                    help="rank 0 (any N): roofline traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes over "
+                         "tools/pmc_probe.py run as child processes on rank 0's GPU after the timed region")
     ap.add_argument("--train", choices=["on", "off"], default="on",
                     help="also time the cfg5 training step (RAFT+DICL ctf-l3, DDP over RCCL when N > 1): "
                          "extra key 'train_step'")
@@ -604,7 +604,22 @@ def corr_leg(args, precision, inputs, world, device, steps, warmup):
     return job_time(elapsed, world, device), ev_gemm, ev_look
 
 
-def live_traffic(args, precision, batch, rank):
+def child_env(device):
+    """Environment of a rank-0 child process that must run on this rank's GPU: HIP_VISIBLE_DEVICES
+    narrowed to it (index into an inherited list, if any), and no torchrun rank variables."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID", "MASTER_ADDR", "MASTER_PORT")}
+    if device is not None and device.type == "cuda":
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+        ids = vis.split(",") if vis else None
+        idx = device.index or 0
+        env["HIP_VISIBLE_DEVICES"] = ids[idx] if ids and idx < len(ids) else str(idx)
+        env.pop("CUDA_VISIBLE_DEVICES", None)
+    return env
+
+
+def live_traffic(args, precision, batch, rank, device=None):
     """HBM bytes per launch of the GEMM and lookup kernels from rocprofv3 PMC counters collected in THIS
     run: separate FETCH_SIZE and WRITE_SIZE passes (one counter group each, MI355X_MICROARCH.md HBM /
     PMC sections) over tools/pmc_probe.py (the same step on the same synthetic inputs), each a child
@@ -627,7 +642,7 @@ def live_traffic(args, precision, batch, rank):
                "--batch", str(batch), "--height", str(args.height), "--width", str(args.width),
                "--channels", str(args.channels), "--iters", str(args.iters)]
         progress(rank, f"live PMC pass {counter} ({precision})")
-        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=d)
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=d, env=child_env(device))
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
             shutil.rmtree(d, ignore_errors=True)
@@ -648,7 +663,8 @@ def live_traffic(args, precision, batch, rank):
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             res[k] = {"read": 2.0 * c["FETCH_SIZE"][0], "write": c["WRITE_SIZE"][0],
                       "total": 2.0 * c["FETCH_SIZE"][0] + c["WRITE_SIZE"][0], "dispatches": c["FETCH_SIZE"][1]}
-    return res, "live: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (KiB -> B, gfx950 correction), this run, tools/pmc_probe.py"
+    return res, ("live: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (KiB -> B, gfx950 correction), this run, tools/pmc_probe.py "
+                 f"on rank {rank}'s GPU")
 
 
 def stored_traffic(precision):
@@ -768,8 +784,10 @@ def main():
         if args.model_level == "on":
             res["model_level"] = model_leg(args, world, rank, device)
     else:
-        live = rank == 0 and world == 1 and args.live_pmc == "on"
-        traffic, note = live_traffic(args, args.precision, B, rank) if live else (None, "")
+        # rank 0 profiles its own GPU in child processes after the timed region (the other ranks go on
+        # to the next leg and wait for rank 0 at its first barrier)
+        live = rank == 0 and args.live_pmc == "on"
+        traffic, note = live_traffic(args, args.precision, B, rank, device) if live else (None, "")
         if traffic is None:
             fallback, fnote = stored_traffic(args.precision)
             traffic, note = fallback, (f"{note}; " if note else "") + fnote
@@ -784,7 +802,7 @@ def main():
             # the parity mode (north_star's fp32 gate) on the same inputs: x3 GEMM + fp32 pyramid
             progress(rank, "fp32_mode leg")
             el32, eg32, el32l = corr_leg(args, "fp32", inputs, world, device, args.fp32_steps, 3)
-            tr32, n32 = live_traffic(args, "fp32", B, rank) if live else (None, "")
+            tr32, n32 = live_traffic(args, "fp32", B, rank, device) if live else (None, "")
             if tr32 is None:
                 fb, fn = stored_traffic("fp32")
                 tr32, n32 = fb, (f"{n32}; " if n32 else "") + fn
@@ -822,11 +840,16 @@ def main():
             res["highres_fs"] = {"error": f"{type(e).__name__}: {e}"[:500]}
         torch.cuda.empty_cache()
     if rank == 0:
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
+            # rank 0 only, after every GPU leg: the other ranks wait at the barrier below
             progress(rank, "cpu_baseline leg")
             res["cpu_baseline"] = cpu_baseline(args)
+            if world > 1:
+                res["cpu_baseline"]["note"] = (f"rank 0 of {world}, timed after every GPU leg while the other ranks "
+                                               f"wait at a barrier")
         print(json.dumps(res), flush=True)
     if world > 1:
+        torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 
 

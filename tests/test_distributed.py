@@ -7,7 +7,9 @@
   driver's): DDP-averaged gradients equal the single-process gradient of the concatenated batch.
 """
 
+import json
 import os
+import subprocess
 import socket
 import sys
 
@@ -197,6 +199,36 @@ def test_bench_model_level_leg_is_batch_sharded(gb):
     assert np.isfinite(ml["rank0_flow_checksum"])
     # both ranks reached the leg (progress lines on stderr)
     assert "rank 0" in out.stderr and "rank 1" in out.stderr and "model_level" in out.stderr
+
+
+def test_bench_rank0_cpu_baseline_at_two_ranks():
+    """N > 1: rank 0 still times the CPU baseline (after every GPU leg, the other ranks waiting at a
+    barrier) and the one JSON line carries it; gloo dry run on the CPU."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--backend",
+                          "gloo", "--steps", "1", "--warmup", "0", "--model-level", "off", "--cpu-budget-s", "0.5"],
+                         capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    cb = res["cpu_baseline"]
+    assert res["n_gpus"] == 2 and cb["value"] > 0 and cb["cores"] >= 1 and "rank 0 of 2" in cb["note"]
+
+
+def test_child_env_pins_rank_gpu():
+    import importlib
+    import torch
+    bench = importlib.import_module("bench")
+    os.environ["HIP_VISIBLE_DEVICES"] = "4,5,6,7"
+    try:
+        env = bench.child_env(torch.device("cuda", 2))
+    finally:
+        del os.environ["HIP_VISIBLE_DEVICES"]
+    assert env["HIP_VISIBLE_DEVICES"] == "6" and "RANK" not in env and "WORLD_SIZE" not in env
+    assert bench.child_env(torch.device("cuda", 1))["HIP_VISIBLE_DEVICES"] == "1"
 
 
 def test_bench_rejects_world_size_mismatch():
