@@ -172,8 +172,9 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * outputs are overwritten (B, C, H, W) float32.  C <= 256.  compute as in rmd_corr_otf_prepare
  * (RMD_F32 and RMD_BF16X3: split-bf16 products, fp32 accumulation; RMD_BF16: bf16 products).
  * Masked and 1-pixel levels and non-finite coordinates record no contribution.  `records` is a host
- * array of `nrecords` device pointers.  Not deterministic (float atomics into the pooled gradient,
- * like ATen's grid_sampler_2d_backward).
+ * array of `nrecords` device pointers.  Deterministic in practice: records are summed in a fixed order,
+ * and the pooled gradient adds per-workgroup fp32 tile sums in fp64 (exact, so order-independent,
+ * while a target's contributions span < 2^29 in magnitude).
  */
 size_t rmd_corr_otf_record_bytes(int batch, int height, int width, int levels, int radius);
 int rmd_corr_otf_record(const float* grad_out, const float* coords, int batch, int height, int width, int levels,

@@ -513,14 +513,17 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
 // two products, so the box of target rows a query tile touches is swept once for all iterations:
 //  * one 512-thread workgroup per 32 x 4 query tile; per level the union box of the tile's patches
 //    over all records, swept in bands of one target row x kBwdTB columns;
-//  * per band the dense G (128 queries x kBwdTB targets, fp32) is summed into LDS from the records
-//    (LDS float atomics: a query's patches of several iterations overlap);
+//  * only the target rows some record patch covers are swept, each over its covered column extent;
+//  * per band the dense G (128 queries x kBwdTB targets, fp32) is built in LDS, one thread per (query,
+//    column) summing the records in order (deterministic);
 //  * d q~ (128 queries x C) += G . P_band: v_mfma_f32_32x32x16_bf16 with A = G rows from LDS and B =
 //    the band's targets in the "T layout" (lane c + 32h holds pixels 8h..8h+7 of channel c of a 16-pixel
 //    segment: the B fragment of a 16-target k-step), accumulated in registers over all bands;
 //  * d P_band (kBwdTB targets x C) = G^T . q~: A = G columns from LDS, B = the tile's queries in the T
-//    layout; the 32 x 32 result tiles go to a pixel-major fp32 d P with float atomics (two 128-B
-//    segments per instruction: the full-rate shape, MI355X_MICROARCH.md §Global float atomics).
+//    layout; the 32 x 32 result tiles (fp32) are added to a pixel-major fp64 d P with float64 atomics:
+//    the fp64 sum of fp32 tile sums is exact — so independent of the order the workgroups add in — as
+//    long as a target's contributions span less than 2^29 in magnitude, and below that the fp64
+//    rounding (2^-53) stays far under the fp32 result's ulp (run-to-run equal in the tests).
 // fp32 modes split G and both operands into bf16 hi + lo and accumulate lo.hi + hi.lo + hi.hi (the
 // forward x3 split); bf16 mode uses one product.
 constexpr int kBwdQX = 32, kBwdQY = 4, kBwdQ = kBwdQX * kBwdQY;
@@ -647,7 +650,7 @@ struct BwdArgs {
     const __bf16* pt;           // targets, T layout (B, TS, ncg units)
     const __bf16* qt;           // queries (fmap1 * scale), T layout (B, QS, ncg units)
     OtfRecords rec;
-    float* dP;                  // (B, PT, C) pixel-major fp32, += G^T q~
+    double* dP;                 // (B, PT, C) pixel-major fp64, += G^T q~ (fp32 tile sums added in fp64)
     long long pT;               // pooled pixels per batch (all levels)
     long long poff[RMD_MAX_LEVELS];
     float* gq;                  // (B, C, H, W) fp32, += scale * G P
@@ -659,7 +662,8 @@ __global__ void __launch_bounds__(kBwdThreads, 1)
 otf_backward_kernel(BwdArgs a) {
     constexpr int K = 2 * R + 2;
     constexpr int NP = X3 ? 2 : 1;
-    extern __shared__ float G[];                                     // [kBwdQ][kBwdLd]
+    extern __shared__ float G[];                                     // [kBwdQ][kBwdLd], then rowext
+    int2* rowext = reinterpret_cast<int2*>(G + kBwdQ * kBwdLd);      // [level-0 rows]
     __shared__ int2 sorg[kMaxRec][kBwdQ];
     __shared__ int box[4];
     const OtfGeom& g = a.g;
@@ -704,27 +708,46 @@ otf_backward_kernel(BwdArgs a) {
         __syncthreads();
         const int bx0 = box[0], bx1 = box[1], by0 = box[2], by1 = box[3];
         if (bx0 > bx1) continue;                                     // uniform: nothing at this level
+        // per target row of the box, the column extent of the record patches that cover it: bands of
+        // rows (and columns) no patch touches are skipped, so a divergent flow costs its patches' rows,
+        // not the whole union box
+        for (int i = tid; i <= by1 - by0; i += kBwdThreads) rowext[i] = make_int2(1 << 30, -(1 << 30));
+        __syncthreads();
+        for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
+            const int2 o = sorg[i / kBwdQ][i % kBwdQ];
+            if (o.x == kFar) continue;
+            const int x0 = max(o.x, 0), x1 = min(o.x + K - 1, lw - 1);
+            for (int j = max(o.y, 0); j <= min(o.y + K - 1, lh - 1); ++j) {
+                atomicMin(&rowext[j - by0].x, x0);
+                atomicMax(&rowext[j - by0].y, x1);
+            }
+        }
+        __syncthreads();
         const __bf16* plev = a.pt + ((size_t)b * g.TS + g.soff[l]) * ncg * unit;
         for (int ty = by0; ty <= by1; ++ty) {
-            for (int cx = bx0 & ~15; cx <= bx1; cx += kBwdTB) {
-                const int ncols = min(kBwdTB, ((bx1 - cx + 1) + 15) & ~15);
-                // ---- G (queries x band targets) from every record's patch row ty ----------------------
+            const int2 ext = rowext[ty - by0];                       // uniform
+            if (ext.x > ext.y) continue;
+            for (int cx = ext.x & ~15; cx <= ext.y; cx += kBwdTB) {
+                const int ncols = min(kBwdTB, ((ext.y - cx + 1) + 15) & ~15);
+                // ---- G (queries x band targets) from every record's patch row ty -----------------------
+                // one thread per (query, column) sums the records in order: deterministic, no atomics;
+                // columns up to the next multiple of 32 are written (zero) for the 32-wide dP tiles
                 __syncthreads();                                     // previous band's G reads done
-                for (int i = tid; i < kBwdQ * kBwdLd; i += kBwdThreads) G[i] = 0.f;
-                __syncthreads();
-                for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
-                    const int r = i / kBwdQ, q = i % kBwdQ;
-                    const int2 o = sorg[r][q];
-                    const int j = ty - o.y;
-                    if (o.x == kFar || j < 0 || j >= K || o.x + K <= cx || o.x >= cx + ncols) continue;
-                    const int y = qy0 + q / kBwdQX, x = qx0 + q % kBwdQX;
-                    const float* wr = a.rec.wp[r] + (((size_t)l * g.B + b) * K * K + j * K) * N + y * g.W + x;
-                    float* grow = G + q * kBwdLd;
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        const int col = o.x + k - cx, tx = o.x + k;
-                        if (col >= 0 && col < ncols && tx >= 0 && tx < lw) atomicAdd(grow + col, wr[(size_t)k * N]);
+                const int ncols32 = (ncols + 31) & ~31;
+                for (int i = tid; i < kBwdQ * ncols32; i += kBwdThreads) {
+                    const int col = i % ncols32, q = i / ncols32;
+                    const int tx = cx + col;
+                    float sum = 0.f;
+                    if (col < ncols && tx < lw) {
+                        const size_t qoff = (size_t)(qy0 + q / kBwdQX) * g.W + qx0 + q % kBwdQX;
+                        for (int r = 0; r < a.rec.n; ++r) {
+                            const int2 o = sorg[r][q];
+                            const int j = ty - o.y, k = tx - o.x;
+                            if (o.x != kFar && j >= 0 && j < K && k >= 0 && k < K)
+                                sum += a.rec.wp[r][(((size_t)l * g.B + b) * K * K + j * K + k) * N + qoff];
+                        }
                     }
+                    G[q * kBwdLd + col] = sum;
                 }
                 __syncthreads();
                 // ---- d q~ += G . P_band (query tile mt, channel tiles nt0..nt0+ntn-1) ------------------
@@ -771,7 +794,7 @@ otf_backward_kernel(BwdArgs a) {
                         }
                     }
                     // lane (channel j32, half h): register 4i + k is target column mt*32 + 8i + 4h + k
-                    float* drow = a.dP + ((size_t)b * a.pT + a.poff[l] + (size_t)ty * lw) * g.C;
+                    double* drow = a.dP + ((size_t)b * a.pT + a.poff[l] + (size_t)ty * lw) * g.C;
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         if (t >= ntn) break;
@@ -780,7 +803,8 @@ otf_backward_kernel(BwdArgs a) {
                         for (int v = 0; v < 16; ++v) {
                             const int col = mt * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
                             const int tx = cx + col;
-                            if (col < ncols && tx <= bx1 && ch < g.C) atomicAdd(drow + (size_t)tx * g.C + ch, accp[t][v]);
+                            if (col < ncols && tx <= ext.y && ch < g.C)
+                                atomicAdd(drow + (size_t)tx * g.C + ch, (double)accp[t][v]);
                         }
                     }
                 }
@@ -808,7 +832,7 @@ otf_backward_kernel(BwdArgs a) {
 // d fmap2[b, c, y, x] = sum_l d P_l[b, (y >> l, x >> l), c] / 4^l over the floor-cropped part of each level
 // (the transpose of l successive 2x2 average pools); one thread per (b, y, x, c), channel fastest.
 __global__ void __launch_bounds__(kThreads)
-otf_unpool_kernel(const float* __restrict__ dP, OtfGeom g, long long pT, LevelOff po, float* __restrict__ gf2) {
+otf_unpool_kernel(const double* __restrict__ dP, OtfGeom g, long long pT, LevelOff po, float* __restrict__ gf2) {
     const long long N = (long long)g.H * g.W;
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
     if (idx >= (long long)g.B * N * g.C) return;
@@ -822,7 +846,7 @@ otf_unpool_kernel(const float* __restrict__ dP, OtfGeom g, long long pT, LevelOf
         if (l >= g.L) break;
         const int yy = y >> l, xx = x >> l;
         if (yy < g.lh[l] && xx < g.lw[l])
-            s += dP[((size_t)b * pT + po.o[l] + (size_t)yy * g.lw[l] + xx) * g.C + c] * (1.0f / (float)(1 << (2 * l)));
+            s += (float)dP[((size_t)b * pT + po.o[l] + (size_t)yy * g.lw[l] + xx) * g.C + c] * (1.0f / (float)(1 << (2 * l)));
     }
     gf2[((size_t)b * g.C + c) * N + p] = s;
 }
@@ -998,7 +1022,7 @@ BwdLayout bwd_layout(int B, int C, int H, int W, int L, int compute) {
     y.pt_off = 0;
     y.qt_off = (tbytes + 255) / 256 * 256;
     y.dp_off = y.qt_off + (qbytes + 255) / 256 * 256;
-    y.total = y.dp_off + (size_t)B * p * C * sizeof(float);
+    y.total = y.dp_off + (size_t)B * p * C * sizeof(double);
     return y;
 }
 
@@ -1052,10 +1076,10 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
     char* ws = static_cast<char*>(workspace);
     __bf16* pt = reinterpret_cast<__bf16*>(ws + y.pt_off);
     __bf16* qt = reinterpret_cast<__bf16*>(ws + y.qt_off);
-    float* dP = reinterpret_cast<float*>(ws + y.dp_off);
+    double* dP = reinterpret_cast<double*>(ws + y.dp_off);
     const size_t N = (size_t)height * width;
     if (hipMemsetAsync(grad_fmap1, 0, (size_t)batch * channels * N * sizeof(float), st) != hipSuccess ||
-        hipMemsetAsync(dP, 0, (size_t)batch * y.pT * channels * sizeof(float), st) != hipSuccess) {
+        hipMemsetAsync(dP, 0, (size_t)batch * y.pT * channels * sizeof(double), st) != hipSuccess) {
         set_error("rmd_corr_otf_backward: hipMemsetAsync failed");
         return RMD_ERR_LAUNCH;
     }
@@ -1086,7 +1110,7 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
     }
     const long long nblk = (long long)((width + kBwdQX - 1) / kBwdQX) * ((height + kBwdQY - 1) / kBwdQY) * batch;
     RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_backward: grid too large");
-    const size_t lds = sizeof(float) * kBwdQ * kBwdLd;
+    const size_t lds = sizeof(float) * kBwdQ * kBwdLd + sizeof(int2) * height;     // G + per-row extents
     const size_t obytes = otf_record_org_bytes(batch, height, width, levels);
     for (int r0 = 0; r0 < nrecords; r0 += kMaxRec) {
         BwdArgs a{};
@@ -1107,7 +1131,7 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
 #define RMD_BWD(XX, RR)                                                                                          \
         do {                                                                                                     \
             auto k = otf_backward_kernel<XX, RR>;                                                                \
-            RMD_REQUIRE(lds <= 160 * 1024, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: %zu B of LDS per block", lds);      \
+            RMD_REQUIRE(lds <= 160 * 1024, RMD_ERR_SHAPE, "rmd_corr_otf_backward: %zu B of LDS per block", lds);    \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                       (int)lds);                                                                 \
             k<<<(unsigned)nblk, kBwdThreads, lds, st>>>(a);                                                      \

@@ -160,7 +160,18 @@ BWD_CASES = [
     (1, 256, 46, 62, 4, 4, 4.0, (), 2),           # cfg1 feature shape
     (1, 16, 30, 50, 2, 7, 25.0, (), 2),           # huge spread: wide union boxes (several bands per row)
     (2, 8, 9, 70, 1, 1, 0.5, (), 35),             # 35 lookups: records split over two launches (32 max)
+    (1, 32, 40, 96, 3, 4, "split", (), 3),        # divergent flow: two patch clusters far apart per query tile
 ]
+
+
+def _case_coords(rng, b, h, w, spread):
+    if spread != "split":
+        return _grid_coords(rng, b, h, w, spread)
+    # left/right halves of every query row pulled 30 columns apart (occlusion-edge-like divergence)
+    co = _grid_coords(rng, b, h, w, 0.5)
+    co[:, 0, :, ::2] += 30.0
+    co[:, 0, :, 1::2] -= 30.0
+    return co
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -174,7 +185,7 @@ def test_otf_backward_matches_oracle(case, precision):
     rng = np.random.default_rng(c * 100 + w)
     f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
     f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
-    cos = [_grid_coords(rng, b, h, w, spread) for _ in range(n)]
+    cos = [_case_coords(rng, b, h, w, spread) for _ in range(n)]
     d = (2 * r + 1) ** 2
     gos = [rng.standard_normal((b, levels * d, h, w)).astype(np.float32) for _ in range(n)]
     _, g1, g2 = _grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, levels, r, precision=precision, method="otf"),
@@ -188,6 +199,23 @@ def test_otf_backward_matches_oracle(case, precision):
         r2 += a2
     assert rel_max_err(g1, r1) < TOL[precision]
     assert rel_max_err(g2, r2) < TOL[precision]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_otf_backward_is_deterministic(precision):
+    """Run-to-run identical gradients (G built in fixed record order, d P summed in fp64): 12 lookups at
+    a cfg1-like map with a spread flow, so many query tiles add into the same pooled targets."""
+    import rmd
+    rng = np.random.default_rng(99)
+    b, c, h, w = 2, 64, 46, 62
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    cos = [_grid_coords(rng, b, h, w, 3.0) for _ in range(12)]
+    gos = [rng.standard_normal((b, 324, h, w)).astype(np.float32) for _ in range(12)]
+    runs = [_grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, 4, 4, precision=precision, method="otf"),
+                   f1, f2, cos, gos)[1:] for _ in range(3)]
+    for g1, g2 in runs[1:]:
+        assert np.array_equal(g1, runs[0][0]) and np.array_equal(g2, runs[0][1])
 
 
 def test_otf_backward_equals_volume_backward_raft_scale():

@@ -6,8 +6,11 @@
 //   tiles4x4 : 4x4 chunks (32 B per slot): per row block i and column group tc two 16-B stores per lane
 //              (halves of its own 4x4 accumulator block), slot stride 32 B
 //   rows1x8  : the round-2 row layout (1x8 chunks, two 512-B runs per instruction after the lane swap)
+//   tiles2x8 : 2x8 chunks (32 B per slot): per chunk row m and column chunk tc one 16-B store per lane,
+//              half-wave h writing bytes 16h..16h+15 of each slot's chunk — one contiguous 1-KiB run per
+//              instruction (round 4 candidate)
 // (a sequential-store reference is tools/hbm_store_bench.hip's seq: 6.3 TB/s)
-// build: hipcc --offload-arch=gfx950 -O3 -o tools/_bin/store_pattern_bench tools/store_pattern_bench.hip
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/_ab/store_pattern_bench tools/store_pattern_bench.hip
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,6 +52,16 @@ __global__ void __launch_bounds__(512, 1) level0_store(unsigned char* __restrict
 #pragma unroll
                     for (int half = 0; half < 2; ++half)
                         __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(pyr + (pos * S + q) * 32 + 16 * half));
+                }
+            }
+        } else if constexpr (MODE == 3) {     // tiles 2x8: TY = 28 chunk rows, TX = 16 chunks of 8 columns
+            for (int m = 0; m < 8; ++m) {
+                const int cr = rb * 8 + m;
+                if (cr >= 28) break;
+#pragma unroll
+                for (int tc = 0; tc < 2; ++tc) {
+                    const size_t pos = ((size_t)b * 28 + cr) * 16 + 2 * cb + tc;
+                    __builtin_nontemporal_store(d, reinterpret_cast<u32x4*>(pyr + (pos * S + q) * 32 + 16 * h));
                 }
             }
         } else if constexpr (MODE == 2) {     // rows 1x8: 55 rows, 16 chunks; lane h writes row 2m + h
@@ -96,6 +109,7 @@ int main() {
         run("tiles2x4", level0_store<0>, b2x4);
         run("tiles4x4", level0_store<1>, b4x4);
         run("rows1x8", level0_store<2>, brow);
+        run("tiles2x8", level0_store<3>, b2x4);
     }
     CK(hipFree(p));
     return 0;
