@@ -84,12 +84,23 @@ __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, in
 #pragma unroll
         for (int i = 0; i < KW; ++i) wd[i] = odd ? __builtin_amdgcn_alignbyte(wd[i + 1], wd[i], 2) : wd[i];
     }
+    if constexpr (MASK) {
+        // zero padding as word masks on the aligned words (element j valid iff 0 <= xs + j < lw and the
+        // row is): row-invariant, so the compiler computes them once per level, in VGPRs — not one
+        // SGPR-pair compare per element and row
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const float e = word_elem<T>(wd[j / EPW], j % EPW);
-        const int col = xs + j;
-        v[j] = (!MASK || (row_ok && col >= 0 && col < lw)) ? e : 0.f;
+        for (int i = 0; i < (K + EPW - 1) / EPW; ++i) {
+            unsigned m;
+            if constexpr (EPW == 2)
+                m = ((unsigned)(xs + 2 * i) < (unsigned)lw ? 0xFFFFu : 0u) |
+                    ((unsigned)(xs + 2 * i + 1) < (unsigned)lw ? 0xFFFF0000u : 0u);
+            else
+                m = (unsigned)(xs + i) < (unsigned)lw ? ~0u : 0u;
+            wd[i] &= row_ok ? m : 0u;
+        }
     }
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = word_elem<T>(wd[j / EPW], j % EPW);
 }
 
 // ---- buffer loads (BUF): image b's slab of a level as one buffer resource -----------------------
@@ -173,7 +184,17 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
 struct OutBuf {
     __amdgpu_buffer_rsrc_t rs;
     unsigned voff;     // p * 4, or kOOB for an inactive lane
+    float* lds;        // XST: the wave's [D][64] output-row staging array
+    unsigned qoff;     // XST: byte offset of pixel (lane & 15)'s quad of 4 pixels, or kOOB
+    bool xst;          // XST: 16-B stores of 4 pixels per lane (needs W % 4 == 0)
 };
+
+#ifndef RMD_LOOKUP_XST
+#define RMD_LOOKUP_XST 0
+#endif
+#ifndef RMD_LOOKUP_H64
+#define RMD_LOOKUP_H64 0
+#endif
 
 __device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, bool active) {
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)o_block);
@@ -188,6 +209,27 @@ __device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, b
 template <int D>
 __device__ __forceinline__ void emit_row_buf(const OutBuf& ob, int N, int bb, float fy, const float (&hprev)[D],
                                              const float (&hcur)[D]) {
+#if RMD_LOOKUP_XST
+    if (ob.xst) {
+        // transpose through LDS: lane l holds plane (l >> 4) + 4k for the 4 pixels of quad l & 15, one
+        // 16-B store per (lane, k) instead of D 4-B stores per lane
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int a = 0; a < D; ++a) ob.lds[a * 64 + lane] = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < (D + 3) / 4; ++k) {
+            const int a = (lane >> 4) + 4 * k;
+            if (k < D / 4 || a < D) {
+                const float4 v = *reinterpret_cast<const float4*>(ob.lds + a * 64 + 4 * (lane & 15));
+                const unsigned off = ob.qoff == kOOB ? kOOB : ob.qoff + (unsigned)((a * D + bb) * N) * 4u;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ob.rs, (int)off, 0, 2);
+            }
+        }
+        __syncthreads();
+        return;
+    }
+#endif
 #pragma unroll
     for (int a = 0; a < D; ++a)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(fmaf(fy, hcur[a] - hprev[a], hprev[a])), ob.rs, (int)ob.voff,
@@ -351,8 +393,33 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
     const int sh = xs - 4 * q0;                                     // 0 .. 3
     const int tys = g.ty[L], txs = g.tx[L];
 
+#if RMD_LOOKUP_H64
+    // A/B: per patch row, NQ 8-B loads straight from the row's half of each chunk (no parity select)
+    unsigned hw[KR][2 * NQ];
+    if constexpr (BUF) {
+        const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
+        const unsigned cs = (unsigned)g.slots * 16u;
+#pragma unroll
+        for (int jj = 0; jj < KR; ++jj) {
+            const int yy = ya + jj;
+            const int crow = floor_div(yy, 2);
+            const bool rneed = crow >= 0 && crow < tys;
+            const unsigned rbase = (unsigned)(crow * txs + q0) * cs + (unsigned)slot * 16u + 8u * (unsigned)(yy - 2 * crow);
+#pragma unroll
+            for (int c = 0; c < NQ; ++c) {
+                const int q = q0 + c;
+                const bool need = rneed && q >= 0 && q < txs && c * 4 < sh + K;
+                unsigned t2[2];
+                buf_words<2>(t2, rs, need ? rbase + (unsigned)c * cs : kOOB);
+                hw[jj][2 * c] = t2[0];
+                hw[jj][2 * c + 1] = t2[1];
+            }
+        }
+    }
+#endif
     unsigned wd[NCR][NQ][4];
     if constexpr (BUF) {
+      if constexpr (!RMD_LOOKUP_H64) {
         const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
         const unsigned cs = (unsigned)g.slots * 16u, rsb = (unsigned)txs * cs;
         const unsigned off00 = (unsigned)(cr0 * txs + q0) * cs + (unsigned)slot * 16u;   // used only when valid
@@ -370,6 +437,7 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
                 for (int i = 0; i < 4; ++i) wd[cr][c][i] = t4[i];
             }
         }
+      }
     } else {
         const int crl = min(max(cr0, 0), tys - 1), ql = min(max(q0, 0), txs - 1);
         const long long cs = (long long)g.slots * 8;                // next quad (elements)
@@ -402,6 +470,13 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
         // parity 0: chunk row jj >> 1, half jj & 1; parity 1: chunk row (jj + 1) >> 1, half (jj + 1) & 1
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
+#if RMD_LOOKUP_H64
+            if constexpr (BUF) {
+                rw[2 * c] = hw[jj][2 * c];
+                rw[2 * c + 1] = hw[jj][2 * c + 1];
+                continue;
+            }
+#endif
             const int r0 = jj >> 1, h0 = (jj & 1) * 2;
             const int r1 = (jj + 1) >> 1, h1 = ((jj + 1) & 1) * 2;
             const unsigned a0 = wd[r0][c][h0], a1 = wd[r0][c][h0 + 1];
@@ -476,6 +551,24 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     float* o = ob_block + p;
     OutBuf ob;
     if constexpr (BUF) ob = out_buf(ob_block, N, D, p, active);
+#if RMD_LOOKUP_XST
+    __shared__ float xlds[D * 64];
+    if constexpr (BUF) {
+        ob.lds = xlds;
+        ob.xst = (g.width & 3) == 0;
+        const int s4 = blockIdx.x * kThreads + 4 * (threadIdx.x & 15);
+        int p4 = s4, ok = s4 < g.slots;
+        if constexpr (LAY == RMD_LAYOUT_TILES) {
+            int y4, x4;
+            tiles_pixel(min(s4, g.slots - 1), g.height, g.width, y4, x4);
+            ok = ok && y4 < g.height && x4 < g.width;
+            p4 = y4 * g.width + x4;
+        } else {
+            ok = ok && s4 < N;
+        }
+        ob.qoff = (ok && (RMD_LOOKUP_ABL & 1) == 0) ? (unsigned)p4 * 4u : kOOB;
+    }
+#endif
     if constexpr (LAY == RMD_LAYOUT_TILES) {
         switch (L) {
             case 0: lookup_level_tiles<R, 0, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;

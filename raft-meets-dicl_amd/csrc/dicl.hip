@@ -1762,8 +1762,18 @@ dap_wgrad_reduce(const float* __restrict__ part, int splits, int D, int Dp, floa
     const int o = ok ? idx / D : 0, i = ok ? idx % D : 0;
     const float* pp = part + (size_t)o * Dp + i;
     const size_t mat = (size_t)Dp * Dp;
+    // the group's partials are summed in split order, 8 loads in flight at a time (the plain loop waited
+    // for each strided load before the next add: latency-bound at ~20 splits per group)
     float s = 0.f;
-    for (int k = gsp; k < splits; k += 16) s += pp[(size_t)k * mat];
+    int k = gsp;
+    for (; k + 16 * 7 < splits; k += 16 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)(k + 16 * u) * mat];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; k += 16) s += pp[(size_t)k * mat];
     red[gsp][i32] = s;
     __syncthreads();
     if (gsp == 0 && ok) {
