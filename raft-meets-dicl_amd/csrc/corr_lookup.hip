@@ -115,6 +115,9 @@ constexpr unsigned kOOB = 0x80000000u;
 #ifndef RMD_LOOKUP_ABL
 #define RMD_LOOKUP_ABL 0
 #endif
+#if RMD_LOOKUP_ABL & 4
+__device__ unsigned g_abl_off = 0x80000000u;
+#endif
 
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const PyrGeom& g, int L, int b) {
@@ -130,6 +133,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const
 template <int NW>
 __device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_rsrc_t rs, unsigned off) {
     if constexpr ((RMD_LOOKUP_ABL & 2) != 0) off = kOOB;
+#if RMD_LOOKUP_ABL & 4
+    off |= g_abl_off;                 // ABL builds: every load to kOOB through a mutable global (not foldable)
+#endif
     if constexpr (NW == 4) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
 #pragma unroll
@@ -184,17 +190,7 @@ __device__ __forceinline__ void load_row(const T* __restrict__ row_ptr, long lon
 struct OutBuf {
     __amdgpu_buffer_rsrc_t rs;
     unsigned voff;     // p * 4, or kOOB for an inactive lane
-    float* lds;        // XST: the wave's [D][64] output-row staging array
-    unsigned qoff;     // XST: byte offset of pixel (lane & 15)'s quad of 4 pixels, or kOOB
-    bool xst;          // XST: 16-B stores of 4 pixels per lane (needs W % 4 == 0)
 };
-
-#ifndef RMD_LOOKUP_XST
-#define RMD_LOOKUP_XST 0
-#endif
-#ifndef RMD_LOOKUP_H64
-#define RMD_LOOKUP_H64 0
-#endif
 
 __device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, bool active) {
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)o_block);
@@ -209,27 +205,6 @@ __device__ __forceinline__ OutBuf out_buf(float* o_block, int N, int D, int p, b
 template <int D>
 __device__ __forceinline__ void emit_row_buf(const OutBuf& ob, int N, int bb, float fy, const float (&hprev)[D],
                                              const float (&hcur)[D]) {
-#if RMD_LOOKUP_XST
-    if (ob.xst) {
-        // transpose through LDS: lane l holds plane (l >> 4) + 4k for the 4 pixels of quad l & 15, one
-        // 16-B store per (lane, k) instead of D 4-B stores per lane
-        const int lane = threadIdx.x & 63;
-#pragma unroll
-        for (int a = 0; a < D; ++a) ob.lds[a * 64 + lane] = fmaf(fy, hcur[a] - hprev[a], hprev[a]);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < (D + 3) / 4; ++k) {
-            const int a = (lane >> 4) + 4 * k;
-            if (k < D / 4 || a < D) {
-                const float4 v = *reinterpret_cast<const float4*>(ob.lds + a * 64 + 4 * (lane & 15));
-                const unsigned off = ob.qoff == kOOB ? kOOB : ob.qoff + (unsigned)((a * D + bb) * N) * 4u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ob.rs, (int)off, 0, 2);
-            }
-        }
-        __syncthreads();
-        return;
-    }
-#endif
 #pragma unroll
     for (int a = 0; a < D; ++a)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(fmaf(fy, hcur[a] - hprev[a], hprev[a])), ob.rs, (int)ob.voff,
@@ -369,13 +344,12 @@ __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, con
     }
 }
 
-// Tiles-layout level 0/1: 2 x 4 fp16 chunks (16 B: row 0 in words 0-1, row 1 in words 2-3).  The
-// part's KR patch rows [ya, ya + KR) span NCR chunk rows from cr0 = floor(ya / 2); patch row jj sits in
-// chunk row (jj + par) >> 1, half (jj + par) & 1 with par = ya & 1 — per lane, so each row's 2 * NQ
-// words are selected between the two parities.  BUF: chunks that are not needed or lie off the level
-// load zeros from kOOB; padding (columns past lw, the odd last row of a chunk row) is masked per
-// element only in waves where some lane's window reaches it (MASK).  !BUF: clamped addresses (an L2
-// hit) and selects.
+// Tiles-layout level 0/1: 2 x 4 fp16 chunks (16 B: row 0 in words 0-1, row 1 in words 2-3).  BUF: each
+// of the part's KR patch rows loads its own 8-B half of NQ chunks; chunks that are not needed or lie off
+// the level (and the padding half of an odd last row) load zeros from kOOB, and padding columns are
+// masked per word only in waves where some lane's window reaches the level's edge (MASK).  !BUF (slabs
+// of 2 GiB and more): whole chunks of NCR chunk rows from clamped addresses (an L2 hit); patch row jj
+// sits in chunk row (jj + par) >> 1, half (jj + par) & 1 with par = ya & 1, selected per lane.
 template <int R, int L, int PR, bool BUF, bool MASK>
 __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const PyrGeom& g, int b, int slot, int N,
                                            float fx, float fy, int xs, int ys, float* __restrict__ o, const OutBuf& ob,
@@ -393,8 +367,8 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
     const int sh = xs - 4 * q0;                                     // 0 .. 3
     const int tys = g.ty[L], txs = g.tx[L];
 
-#if RMD_LOOKUP_H64
-    // A/B: per patch row, NQ 8-B loads straight from the row's half of each chunk (no parity select)
+    // BUF: per patch row, NQ 8-B loads straight from the row's half of each chunk (no parity select;
+    // 64 VGPRs vs 72 for whole-chunk loads + selects, 1-2 % faster, profiles/lookup_ab_r04.json)
     unsigned hw[KR][2 * NQ];
     if constexpr (BUF) {
         const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
@@ -403,7 +377,7 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
         for (int jj = 0; jj < KR; ++jj) {
             const int yy = ya + jj;
             const int crow = floor_div(yy, 2);
-            const bool rneed = crow >= 0 && crow < tys;
+            const bool rneed = crow >= 0 && crow < tys && yy < lh;      // the odd last row's padding half: zeros
             const unsigned rbase = (unsigned)(crow * txs + q0) * cs + (unsigned)slot * 16u + 8u * (unsigned)(yy - 2 * crow);
 #pragma unroll
             for (int c = 0; c < NQ; ++c) {
@@ -416,29 +390,8 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
             }
         }
     }
-#endif
     unsigned wd[NCR][NQ][4];
-    if constexpr (BUF) {
-      if constexpr (!RMD_LOOKUP_H64) {
-        const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
-        const unsigned cs = (unsigned)g.slots * 16u, rsb = (unsigned)txs * cs;
-        const unsigned off00 = (unsigned)(cr0 * txs + q0) * cs + (unsigned)slot * 16u;   // used only when valid
-#pragma unroll
-        for (int cr = 0; cr < NCR; ++cr) {
-            const int crow = cr0 + cr;
-            const bool rneed = crow >= 0 && crow < tys && 2 * cr <= par + KR - 1;
-#pragma unroll
-            for (int c = 0; c < NQ; ++c) {
-                const int q = q0 + c;
-                const bool need = rneed && q >= 0 && q < txs && c * 4 < sh + K;
-                unsigned t4[4];
-                buf_words<4>(t4, rs, need ? off00 + (unsigned)cr * rsb + (unsigned)c * cs : kOOB);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) wd[cr][c][i] = t4[i];
-            }
-        }
-      }
-    } else {
+    if constexpr (!BUF) {
         const int crl = min(max(cr0, 0), tys - 1), ql = min(max(q0, 0), txs - 1);
         const long long cs = (long long)g.slots * 8;                // next quad (elements)
         const __half* base = pyr + g.off[L] + (long long)slot * 8;
@@ -470,13 +423,11 @@ __device__ __forceinline__ void tiles_body(const __half* __restrict__ pyr, const
         // parity 0: chunk row jj >> 1, half jj & 1; parity 1: chunk row (jj + 1) >> 1, half (jj + 1) & 1
 #pragma unroll
         for (int c = 0; c < NQ; ++c) {
-#if RMD_LOOKUP_H64
             if constexpr (BUF) {
                 rw[2 * c] = hw[jj][2 * c];
                 rw[2 * c + 1] = hw[jj][2 * c + 1];
                 continue;
             }
-#endif
             const int r0 = jj >> 1, h0 = (jj & 1) * 2;
             const int r1 = (jj + 1) >> 1, h1 = ((jj + 1) & 1) * 2;
             const unsigned a0 = wd[r0][c][h0], a1 = wd[r0][c][h0 + 1];
@@ -522,8 +473,16 @@ __device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ py
 }
 
 // grid: (slot blocks of 64, batch, level + levels * part) — one lane per (query slot, level, row part)
+#ifndef RMD_LOOKUP_WPE8
+#define RMD_LOOKUP_WPE8 0
+#endif
+#if RMD_LOOKUP_WPE8
+#define RMD_LOOKUP_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define RMD_LOOKUP_ATTR
+#endif
 template <typename T, int R, int PR, int LAY, bool BUF>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads) RMD_LOOKUP_ATTR
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
     const int N = g.height * g.width;
@@ -551,24 +510,6 @@ corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict
     float* o = ob_block + p;
     OutBuf ob;
     if constexpr (BUF) ob = out_buf(ob_block, N, D, p, active);
-#if RMD_LOOKUP_XST
-    __shared__ float xlds[D * 64];
-    if constexpr (BUF) {
-        ob.lds = xlds;
-        ob.xst = (g.width & 3) == 0;
-        const int s4 = blockIdx.x * kThreads + 4 * (threadIdx.x & 15);
-        int p4 = s4, ok = s4 < g.slots;
-        if constexpr (LAY == RMD_LAYOUT_TILES) {
-            int y4, x4;
-            tiles_pixel(min(s4, g.slots - 1), g.height, g.width, y4, x4);
-            ok = ok && y4 < g.height && x4 < g.width;
-            p4 = y4 * g.width + x4;
-        } else {
-            ok = ok && s4 < N;
-        }
-        ob.qoff = (ok && (RMD_LOOKUP_ABL & 1) == 0) ? (unsigned)p4 * 4u : kOOB;
-    }
-#endif
     if constexpr (LAY == RMD_LAYOUT_TILES) {
         switch (L) {
             case 0: lookup_level_tiles<R, 0, PR, BUF>(pyr, g, b, slot, N, x, y, zmask, o, ob, active, part); break;

@@ -436,3 +436,27 @@ def test_large_batch_offsets_vs_oracle(precision):
         cos = co[bi:bi + 1].reshape(1, 2, n)[:, :, sel][:, :, None, :].double().numpy()
         ref = oracle.corr_lookup(oracle.corr_pyramid(f1s, f2[bi:bi + 1].double().numpy(), 4), cos, 4)
         assert rel_max_err(got, ref.reshape(324, -1)) < TOL[precision], f"image {bi}"
+
+
+def test_pyramid_tensor_carries_its_layout_48x64():
+    """at an even shape (48x64, C=256, bf16) the row and tiles descs of the pyramid have the
+    same element count, so a layout flag the caller passes could silently scramble the lookup.  The
+    pyramid tensor carries its layout in its shape instead: the w8 GEMM's tiles pyramid is (n, 8), the
+    lookup reads it correctly, and any other 2-D view is rejected."""
+    import rmd
+    from rmd import _lib
+    rng = np.random.default_rng(48)
+    f1 = rng.standard_normal((1, 256, 48, 64)).astype(np.float32)
+    f2 = rng.standard_normal((1, 256, 48, 64)).astype(np.float32)
+    ys, xs = np.meshgrid(np.arange(48), np.arange(64), indexing="ij")
+    co = (np.stack([xs, ys])[None] + rng.normal(0, 2, (1, 2, 48, 64))).astype(np.float32)
+    rows = _lib.describe(1, 48, 64, 4, _lib.RMD_F16, _lib.RMD_LAYOUT_ROWS)
+    tiles = _lib.describe(1, 48, 64, 4, _lib.RMD_F16, _lib.RMD_LAYOUT_TILES)
+    assert rows.total_elements == tiles.total_elements            # the ambiguous case
+    pyr = torch.ops.rmd.corr_pyramid(_t(f1), _t(f2), 4, _lib.RMD_BF16, _lib.RMD_F16, 1 / 16)
+    assert pyr.shape == (tiles.total_elements // 8, 8)
+    out = torch.ops.rmd.corr_lookup(pyr, _t(co), 4, 4, 0).cpu().numpy()
+    ref = oracle.corr_lookup(oracle.corr_pyramid(f1.astype(np.float64), f2.astype(np.float64), 4), co.astype(np.float64), 4)
+    assert rel_max_err(out, ref) < TOL["bf16"]
+    with pytest.raises(ValueError, match="tiles layout"):
+        torch.ops.rmd.corr_lookup(pyr.view(-1, 16), _t(co), 4, 4, 0)

@@ -83,9 +83,10 @@ def test_opcheck_operator_families():
     ]
     for op, args in cases:
         torch.library.opcheck(op, args, test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
-    pyr = torch.ops.rmd.corr_pyramid(f1.detach(), f2.detach(), 3, _lib.RMD_BF16X3, _lib.RMD_F32, 0.25)
-    torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0, _lib.RMD_LAYOUT_ROWS),
-                          test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
+    for compute, storage in ((_lib.RMD_BF16X3, _lib.RMD_F32), (_lib.RMD_BF16, _lib.RMD_F16)):     # rows, tiles
+        pyr = torch.ops.rmd.corr_pyramid(f1.detach(), f2.detach(), 3, compute, storage, 0.25)
+        torch.library.opcheck(torch.ops.rmd.corr_lookup, (pyr, co, 3, 2, 0),
+                              test_utils=("test_schema", "test_autograd_registration", "test_faketensor"))
 
 
 @pytest.mark.parametrize("kind,fixture", [("dicl", "dicl_b1_c16_8x12"), ("dicl-1x1", "dicl1x1_b2_c16_8x12"),

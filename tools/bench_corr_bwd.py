@@ -5,7 +5,8 @@ rmd.raft.CorrBlock with feature maps that require gradients: the pyramid (GEMM +
 12 lookups, then autograd: 12 rmd_corr_lookup_backward into the dense query-minor G, the pooled
 target features, two GEMMs and the unpool kernel.  Shape: FlyingChairs 368x496 -> 46x62 (RAFT pads
 modulo 8), C = 256, batch 6 (SURVEY.md §8(d) cfg5 batch), smooth moving coordinates.
-usage: bench_corr_bwd.py [reps] [precision]   -> one JSON document on stdout
+usage: bench_corr_bwd.py [reps] [precision] [cfg5|cfg2]   -> one JSON document on stdout
+(cfg2: bench.py's headline shape, 55x128, batch 8)
 """
 import json
 import os
@@ -24,8 +25,9 @@ def main():
     import rmd
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+    shape = sys.argv[3] if len(sys.argv) > 3 else "cfg5"
     dev = torch.device("cuda", 0)
-    b, c, h, w = 6, 256, 46, 62
+    b, c, h, w = (8, 256, 55, 128) if shape == "cfg2" else (6, 256, 46, 62)
     f1, f2, coords = bench.synthetic(b, c, h, w, 12, 1234, dev)
     f1.requires_grad_(True)
     f2.requires_grad_(True)
