@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
 sys.path.insert(0, ROOT)
 
-MODES = ["bench", "nogemm", "oneout", "samecoord"]
+MODES = os.environ.get("LOOKUP_CONTEXT_MODES", "bench,nogemm,oneout,samecoord").split(",")
 
 
 def run(steps):
@@ -66,9 +66,10 @@ def summary(path):
     groups = [g for g in groups if any("corr_lookup" in n for _, _, n in g)][-len(MODES):]
     res = {}
     for mode, g in zip(MODES, groups):
-        pos, k = {}, None
+        pos, k, gemm = {}, None, []
         for s, e, n in g:
             if "corr_pyramid" in n:
+                gemm.append((e - s) / 1e3)
                 k = 0
             elif "corr_lookup" in n:
                 k = 0 if k is None else k
@@ -77,6 +78,9 @@ def summary(path):
         res[mode] = {p: round(st.median(v[2:] if len(v) > 4 else v), 2) for p, v in sorted(pos.items())}
         allv = [x for v in pos.values() for x in (v[2:] if len(v) > 4 else v)]
         res[mode]["mean"] = round(sum(allv) / len(allv), 2)
+        if len(gemm) > 4:
+            res[mode]["gemm"] = round(st.median(gemm[2:]), 2)
+            res[mode]["gemm_plus_12"] = round(res[mode]["gemm"] + 12 * res[mode]["mean"], 1)
     print(json.dumps(res))
 
 
