@@ -30,6 +30,7 @@
 #include "rmd_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rmd {
 namespace {
@@ -71,6 +72,21 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #endif
 #ifndef RMD_OTF_QL_X
 #define RMD_OTF_QL_X 0
+#endif
+// LDS write of a task's products (put): 1 = every lane writes its 4 products, those outside its query's
+// patch into a pad slot (no branches), 0 = only the products inside, under per-element branches.
+// cfg2 A/B (profiles/otf_put_ab_r04.json): bf16 70.8-73.2 us with 1 vs 75.9-78.5 with 0; split-bf16
+// (two waves per SIMD) 150 with 0 vs 170 with 1
+#ifndef RMD_OTF_PUTSEL_B
+#define RMD_OTF_PUTSEL_B 1
+#endif
+#ifndef RMD_OTF_PUTSEL_X
+#define RMD_OTF_PUTSEL_X 0
+#endif
+// pad slots per query patch in LDS (odd patch stride): 1, or 4 = one per lane group (put's pad writes of
+// the 4 lane groups of a query go to distinct addresses)
+#ifndef RMD_OTF_PADS
+#define RMD_OTF_PADS 1
 #endif
 // ablation for A/B timing only (wrong results): 1 = no output stores
 #ifndef RMD_OTF_ABL
@@ -246,6 +262,9 @@ __device__ __forceinline__ void seg_mma(f32x4& acc, const typename Seg<T>::frag*
 // load each target segment of their box once for more queries (the L2 -> CU operand traffic is the
 // bound: every block re-reads its box), at the cost of MFMA tiles for targets outside a query's own
 // window.  A 16 x 4 block (bf16) reads 2.5x fewer target bytes per query than 16 x 2.
+// LDS floats per query patch: the (2r+2)^2 products, then RMD_OTF_PADS pad slots, rounded to an odd stride
+constexpr int otf_patch_stride(int R) { return ((2 * R + 2) * (2 * R + 2) + RMD_OTF_PADS) | 1; }
+
 template <int QSX, int QSY> struct QBlock {
     static constexpr int kQS = QSX * QSY, kBX = 16 * QSX, kBY = QSY, kQ = kBX * kBY;
 };
@@ -263,7 +282,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     using QB = QBlock<QSX, QSY>;
     constexpr int kQS = QB::kQS, kBX = QB::kBX, kBY = QB::kBY, kQ = QB::kQ;
     constexpr int kWaves = kLookThreads / 64;
-    constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = KK + 1;   // odd patch stride: queries spread over banks
+    constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = otf_patch_stride(R);   // odd: queries spread over banks
+    constexpr bool kPutSel = sizeof(T) == 2 && !X3 ? RMD_OTF_PUTSEL_B != 0 : RMD_OTF_PUTSEL_X != 0;
     extern __shared__ float S[];                       // [kQ][KKp]: every query's (2r+2)^2 patch
     // every level's window origins / fractions and the block's bounding box per level, computed once
     // before the level loop (no per-level reduction barriers)
@@ -277,7 +297,8 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
     const int qb = lid % nqb, b = lid / nqb;
     const int qx0 = (qb % nbx) * kBX, qy0 = (qb / nbx) * kBY;
     const int N = g.H * g.W;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: task indices in SGPRs
     constexpr int NP = X3 ? 2 : 1;                      // load steps per channel step (X3: hi, lo)
     const int cp = CPT > 0 ? CPT : g.Cp;
     const int nls = cp / SG::LSC;
@@ -384,27 +405,40 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 wy[s] = sys[L][wq[s]];
             }
             __syncthreads();
-            // C[target 4*(lane>>4)+e][query lane&15] of task (box row, segment): keep the products inside
-            // the query's own patch
-            auto put = [&](const f32x4& acc, int s, int task) {
-                const int r = task / nseg;
+            // C[target 4*(lane>>4)+e][query lane&15] of task (box row r, target segment column c): keep the
+            // products inside the query's own patch (kPutSel: the others go to a pad slot of the query,
+            // never read, so the four LDS writes carry no branches)
+            auto put = [&](const f32x4& acc, int s, int r, int c) {
                 const int dy = by0 + r - wy[s];
-                const int dx0 = (sa + task - r * nseg) * 16 + 4 * (lane >> 4) - wx[s];
-                if ((unsigned)dy < (unsigned)K) {
-                    float* P = S + wq[s] * KKp + dy * K;
+                const int dx0 = c * 16 + 4 * (lane >> 4) - wx[s];
+                const bool rok = (unsigned)dy < (unsigned)K;
+                float* P = S + wq[s] * KKp;
+                if constexpr (kPutSel) {
+                    const int pad = KK + (RMD_OTF_PADS > 1 ? (lane >> 4) % RMD_OTF_PADS : 0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) P[rok && (unsigned)(dx0 + e) < (unsigned)K ? dy * K + dx0 + e : pad] = acc[e];
+                } else if (rok) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if ((unsigned)(dx0 + e) < (unsigned)K) P[dx0 + e] = acc[e];
+                        if ((unsigned)(dx0 + e) < (unsigned)K) P[dy * K + dx0 + e] = acc[e];
                 }
             };
-            auto tptr = [&](int task) {
-                const int r = task / nseg;
-                return tlev + ((size_t)(by0 + r) * g.nsx[L] + sa + task - r * nseg) * segsz + (size_t)lane * SG::LE;
+            auto tptr = [&](int r, int c) {
+                return tlev + ((size_t)(by0 + r) * g.nsx[L] + c) * segsz + (size_t)lane * SG::LE;
+            };
+            // the wave's tasks w, w + kWaves, ... as (box row, segment column), advanced without division
+            int tr = w / nseg, tcol = sa + w - tr * nseg;
+            auto advance = [&](int& r, int& c) {
+                c += kWaves;
+                while (c >= sa + nseg) {
+                    c -= nseg;
+                    ++r;
+                }
             };
             if constexpr (CPT > 0) {
-                for (int task = w; task < ntask; task += kWaves) {
+                for (int task = w; task < ntask; task += kWaves, advance(tr, tcol)) {
                     frag tc[NLS];
-                    const T* tsb = tptr(task);
+                    const T* tsb = tptr(tr, tcol);
 #pragma unroll
                     for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
 #pragma unroll
@@ -416,12 +450,12 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                             qget(u, s, ls);
                             seg_mma<T, X3>(acc, tc + ls, u);
                         }
-                        put(acc, s, task);
+                        put(acc, s, tr, tcol);
                     }
                 }
             } else {
-                for (int task = w; task < ntask; task += kWaves) {
-                    const T* tsb = tptr(task);
+                for (int task = w; task < ntask; task += kWaves, advance(tr, tcol)) {
+                    const T* tsb = tptr(tr, tcol);
                     f32x4 acc[kQS];
 #pragma unroll
                     for (int s = 0; s < kQS; ++s) acc[s] = f32x4{};
@@ -439,7 +473,7 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                         }
                     }
 #pragma unroll
-                    for (int s = 0; s < kQS; ++s) put(acc[s], s, task);
+                    for (int s = 0; s < kQS; ++s) put(acc[s], s, tr, tcol);
                 }
             }
             __syncthreads();
@@ -940,7 +974,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         auto k = otf_lookup_kernel<T, XS, RR, CC, QX, QY, OC, QLK, NTK>;                                        \
         const long long nblk = (long long)((width + QB::kBX - 1) / QB::kBX) * ((height + QB::kBY - 1) / QB::kBY) * batch; \
         RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");                  \
-        const size_t lds = sizeof(float) * QB::kQ * ((2 * RR + 2) * (2 * RR + 2) + 1) +                      \
+        const size_t lds = sizeof(float) * QB::kQ * otf_patch_stride(RR) +                      \
                            (QLK && CC > 0 ? (size_t)QB::kQS * 16 * CC * XN * sizeof(T) : 0);                    \
         RMD_REQUIRE(lds <= 160 * 1024, RMD_ERR_SHAPE, "rmd_corr_otf_lookup: %zu B of LDS per block", lds);      \
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
