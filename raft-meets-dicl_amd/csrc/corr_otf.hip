@@ -71,7 +71,7 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #define RMD_OTF_QL_B 1
 #endif
 #ifndef RMD_OTF_QL_X
-#define RMD_OTF_QL_X 0
+#define RMD_OTF_QL_X 1
 #endif
 // LDS write of a task's products (put): 1 = every lane writes its 4 products, those outside its query's
 // patch into a pad slot (no branches), 0 = only the products inside, under per-element branches.
@@ -83,12 +83,17 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_PUTSEL_X
 #define RMD_OTF_PUTSEL_X 0
 #endif
+// MFMA order in a task: 1 = load step outer, query segments inner (independent chains interleaved)
+#ifndef RMD_OTF_ILV
+#define RMD_OTF_ILV 1
+#endif
 // pad slots per query patch in LDS (odd patch stride): 1, or 4 = one per lane group (put's pad writes of
 // the 4 lane groups of a query go to distinct addresses)
 #ifndef RMD_OTF_PADS
 #define RMD_OTF_PADS 1
 #endif
-// ablation for A/B timing only (wrong results): 1 = no output stores
+// ablation for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks, 3 = tasks
+// without MFMAs (operand loads and puts), 4 = tasks without operand loads (MFMAs on one task's operands)
 #ifndef RMD_OTF_ABL
 #define RMD_OTF_ABL 0
 #endif
@@ -436,21 +441,50 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
                 }
             };
             if constexpr (CPT > 0) {
-                for (int task = w; task < ntask; task += kWaves, advance(tr, tcol)) {
-                    frag tc[NLS];
-                    const T* tsb = tptr(tr, tcol);
+                frag tc[NLS];
+                if constexpr (RMD_OTF_ABL == 4) {          // ablation: one task's operands for all tasks
+                    const T* tsb = tptr(by0, sa);
 #pragma unroll
                     for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                }
+                for (int task = w; task < (RMD_OTF_ABL == 2 ? 0 : ntask); task += kWaves, advance(tr, tcol)) {
+                    if constexpr (RMD_OTF_ABL != 4) {
+                        const T* tsb = tptr(tr, tcol);
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ++ls) tc[ls] = *reinterpret_cast<const frag*>(tsb + (size_t)ls * 64 * SG::LE);
+                    }
+                    if constexpr (RMD_OTF_ILV && RMD_OTF_ABL != 3) {
+                        // load step outer, query segment inner: kQS independent accumulator chains interleave
+                        f32x4 acc[kQS];
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) acc[s] = f32x4{};
+#pragma unroll
+                        for (int ls = 0; ls < NLS; ls += NP)
+#pragma unroll
+                            for (int s = 0; s < kQS; ++s) {
+                                frag u[NP];
+                                qget(u, s, ls);
+                                seg_mma<T, X3>(acc[s], tc + ls, u);
+                            }
+#pragma unroll
+                        for (int s = 0; s < kQS; ++s) put(acc[s], s, tr, tcol);
+                    } else {
 #pragma unroll
                     for (int s = 0; s < kQS; ++s) {
                         f32x4 acc = {};
+                        if constexpr (RMD_OTF_ABL == 3) {      // ablation: operand loads and puts, no MFMA
 #pragma unroll
-                        for (int ls = 0; ls < NLS; ls += NP) {
-                            frag u[NP];
-                            qget(u, s, ls);
-                            seg_mma<T, X3>(acc, tc + ls, u);
+                            for (int ls = 0; ls < NLS; ++ls) acc[ls & 3] += (float)tc[ls][s & 7];
+                        } else {
+#pragma unroll
+                            for (int ls = 0; ls < NLS; ls += NP) {
+                                frag u[NP];
+                                qget(u, s, ls);
+                                seg_mma<T, X3>(acc, tc + ls, u);
+                            }
                         }
                         put(acc, s, tr, tcol);
+                    }
                     }
                 }
             } else {
