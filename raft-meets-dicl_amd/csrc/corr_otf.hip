@@ -41,14 +41,16 @@ constexpr int kThreads = 256;                        // prepare kernels
 #define RMD_OTF_NT_B 256
 #endif
 #ifndef RMD_OTF_NT_X
-#define RMD_OTF_NT_X 256
+#define RMD_OTF_NT_X 512
 #endif
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block, occupancy and query-fragment placement per compute (-D knobs for A/B builds,
 // tools/_gpu_r03k.sh).  cfg2 bf16, one box per comparison (profiles/otf_patch_ab_r03.jsonl,
 // otf_ql_ab_r03.jsonl): 16x2 blocks with the query fragments in LDS (QL) 77.7 us; 16x1 with them in
-// registers 87.5; 16x4 in registers 84.8; 16x4 QL 100.7 at 256 threads, 77.2 at 512.  Split-bf16 keeps
-// 16x2 with register fragments (203 us; QL 303: three MFMAs per LDS fragment pair read).
+// registers 87.5; 16x4 in registers 84.8; 16x4 QL 100.7 at 256 threads, 77.2 at 512.  Round 4, with the
+// interleaved MFMA order (profiles/otf_put_ab_r04.json): bf16 16x2 QL 256 threads 69-71 us (16x4 at 512
+// 73-74, 16x1 88-91, 16x2 at 512 / 384 / 128 threads 75 / 86 / 83); split-bf16 16x2 QL 512 threads
+// 115-119 us (256 threads 136-139, register fragments 145-147).
 #ifndef RMD_OTF_QSX_B
 #define RMD_OTF_QSX_B 1
 #endif
