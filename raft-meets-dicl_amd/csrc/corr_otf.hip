@@ -43,6 +43,7 @@ constexpr int kThreads = 256;                        // prepare kernels
 #ifndef RMD_OTF_NT_X
 #define RMD_OTF_NT_X 512
 #endif
+constexpr long long kWideBlocks = 4096;              // bf16: 16x4 query blocks from this many 16x2 blocks
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block, occupancy and query-fragment placement per compute (-D knobs for A/B builds,
 // tools/_gpu_r03k.sh).  cfg2 bf16, one box per comparison (profiles/otf_patch_ab_r03.jsonl,
@@ -1037,7 +1038,17 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         case 7: RMD_OTF_C(T, 7, QX, QY, OC); break;                  \
         default: RMD_OTF_C(T, 8, QX, QY, OC); break;                 \
     }
-    if (compute == RMD_BF16) {
+    // bf16 on wide maps (at least kWideBlocks 16x2 query blocks): 16x4 blocks at 512 threads read 45 %
+    // fewer target bytes per query; at the 4K map (b2, 270x480) 362 us vs 396 us per lookup, at cfg2
+    // (1,792 blocks) 77 vs 73 us (profiles/otf_put_ab_r04.json, box r04t)
+    const long long blocks16x2 = (long long)((width + 15) / 16) * ((height + 1) / 2) * batch;
+    if (compute == RMD_BF16 && blocks16x2 >= kWideBlocks) {
+        constexpr bool XS = false;
+        constexpr size_t XN = 1;
+        constexpr bool QLK = true;
+        constexpr int NTK = 512;
+        RMD_OTF_R(__bf16, 1, 4, 2)
+    } else if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool QLK = RMD_OTF_QL_B != 0;
@@ -1053,7 +1064,7 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool QLK = false;
-        constexpr int NTK = RMD_OTF_NT_X;
+        constexpr int NTK = 256;
         RMD_OTF_R(float, RMD_OTF_QSX_X, RMD_OTF_QSY_X, 1)
     }
 #undef RMD_OTF_R

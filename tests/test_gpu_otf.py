@@ -125,6 +125,28 @@ def test_otf_full_size_agrees_with_volume_path(precision):
     assert rel_max_err(a.cpu().numpy(), ref.cpu().numpy()) < TOL[precision]
 
 
+def test_otf_wide_map_agrees_with_volume_path():
+    """bf16 on a wide map (B=4, 128x256: 4,096 16x2 query blocks) takes the 16x4-block kernel
+    (csrc/corr_otf.hip kWideBlocks); it must equal the pyramid + lookup within the bf16 tolerance, with
+    large and small displacements, and be deterministic."""
+    import rmd
+    g = torch.Generator(device="cpu").manual_seed(11)
+    f1 = torch.randn(4, 256, 128, 256, generator=g).to(DEV)
+    f2 = torch.randn(4, 256, 128, 256, generator=g).to(DEV)
+    ys, xs = torch.meshgrid(torch.arange(128.0), torch.arange(256.0), indexing="ij")
+    co = torch.stack([xs, ys])[None] + 6 * torch.randn(4, 2, 128, 256, generator=g)
+    co[1] += 40.0                                      # one image with a large shift (boxes off the map)
+    co = co.to(DEV)
+    otf = rmd.raft_fs.CorrBlock(f1, f2, 4, 4, precision="bf16", method="otf")
+    a = otf(co)
+    b = otf(co)
+    vol = rmd.raft_fs.CorrBlock(f1, f2, 4, 4, precision="fp32")
+    ref = vol(co)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert rel_max_err(a.cpu().numpy(), ref.cpu().numpy()) < TOL["bf16"]
+
+
 def _grads(cb_factory, f1, f2, coords_list, gouts, mask=()):
     t1 = _t(f1).requires_grad_(True)
     t2 = _t(f2).requires_grad_(True)

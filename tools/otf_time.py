@@ -2,7 +2,7 @@
 """Per-lookup time of the on-the-fly lookup (rmd_corr_otf_lookup) at cfg2 (B=8, 55x128, C=256, 4 levels,
 r=4) on bench.py's synthetic coordinates, HIP events around each of 12 lookups x reps; run it once per
 library build (RMD_LIBRARY=...) on one box for an A/B.  Prints one JSON line.
-usage: python3 tools/otf_time.py [reps] [precision ...]"""
+usage: python3 tools/otf_time.py [reps] [precision ...]; OTF_SHAPE=B,H,W overrides the map (4K: 2,270,480)"""
 import json
 import os
 import sys
@@ -19,8 +19,9 @@ from rmd import ops  # noqa: E402
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     precs = sys.argv[2:] or ["bf16", "fp32"]
-    f1, f2, coords = bench.synthetic(8, 256, 55, 128, 12, 1234, "cuda")
-    res = {"lib": os.environ.get("RMD_LIBRARY", "librmd.so")}
+    b, h, w = (int(v) for v in os.environ.get("OTF_SHAPE", "8,55,128").split(","))
+    f1, f2, coords = bench.synthetic(b, 256, h, w, 12, 1234, "cuda")
+    res = {"lib": os.environ.get("RMD_LIBRARY", "librmd.so"), "shape": [b, 256, h, w]}
     for p in precs:
         st = ops.otf_prepare(f1, f2, 4, p, scale=1.0)
         for i in range(12):
