@@ -24,7 +24,9 @@
 //   over its (2r+2)^2 integer patch with the forward's bilinear weights (separable: x then y) and
 //   read-modify-writes the patch — no atomics: the patch rows are split over 3 lanes (parts) that
 //   write disjoint rows, no other lane touches column p, and successive lookups are ordered by the
-//   stream.
+//   stream.  Since the lane owns every (chunk, p) piece its rows touch, it reads, adds to and writes
+//   whole 32-B pieces as two 16-B vectors (the row's values barrel-shifted to their slots): 77 vs 143 us
+//   per cfg2 b8 lookup backward for one float per target (profiles/raft_bwd_vec_ab_r04.json).
 
 #include "rmd_common.h"
 
@@ -34,6 +36,10 @@ namespace {
 constexpr int kThreads = 256;
 
 constexpr int kGcw = 8;                // targets per G chunk
+// lookup backward: 1 = read-modify-write whole 32-B chunk pieces as 16-B vectors, 0 = one float per target
+#ifndef RMD_BWD_VEC
+#define RMD_BWD_VEC 1
+#endif
 
 struct GradGeom {
     int batch, height, width, levels;
@@ -118,10 +124,48 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
         const int y = ys + j;
         if (y >= 0 && y < lh) {
             float* r = col + (size_t)y * g.nch[L] * chs;
+            if constexpr (RMD_BWD_VEC) {
+                // whole 32-B chunk pieces: the row's K values shifted to their in-chunk slots (a 3-stage
+                // barrel shift by xs mod 8), then each chunk the row touches read, added to and written as
+                // two 16-B vectors (the lane owns (chunk, query) for this launch: no other lane writes it);
+                // slots outside the window or past the level's width add 0
+                constexpr int NC = (K + 14) / 8, NW = 8 * NC;
+                float wv[NW];
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const int x = xs + i;
-                if (x >= 0 && x < lw) r[(size_t)(x >> 3) * chs + (x & 7)] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                for (int i = 0; i < NW; ++i) wv[i] = i < K ? qcur[i] * (1.0f - fy) + qprev[i] * fy : 0.f;
+                const int sh = xs & 7;
+#pragma unroll
+                for (int st = 1; st < 8; st <<= 1) {
+                    const bool on = (sh & st) != 0;
+#pragma unroll
+                    for (int i = NW - 1; i >= 0; --i) wv[i] = on ? (i >= st ? wv[i - st] : 0.f) : wv[i];
+                }
+                const int c0 = xs >> 3, nch = g.nch[L];
+                const int nc = (sh + K + 7) >> 3;                       // chunks this row spans (2 or 3 at r = 4)
+#pragma unroll
+                for (int k = 0; k < NC; ++k) {
+                    const int c = c0 + k;
+                    if (k >= nc || c < 0 || c >= nch) continue;
+                    float4* pc = reinterpret_cast<float4*>(r + (size_t)c * chs);
+                    float4 a = pc[0], b = pc[1];
+                    const int lim = lw - 8 * c;                         // slots e < lim are on the level
+                    a.x += 0 < lim ? wv[8 * k + 0] : 0.f;
+                    a.y += 1 < lim ? wv[8 * k + 1] : 0.f;
+                    a.z += 2 < lim ? wv[8 * k + 2] : 0.f;
+                    a.w += 3 < lim ? wv[8 * k + 3] : 0.f;
+                    b.x += 4 < lim ? wv[8 * k + 4] : 0.f;
+                    b.y += 5 < lim ? wv[8 * k + 5] : 0.f;
+                    b.z += 6 < lim ? wv[8 * k + 6] : 0.f;
+                    b.w += 7 < lim ? wv[8 * k + 7] : 0.f;
+                    pc[0] = a;
+                    pc[1] = b;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const int x = xs + i;
+                    if (x >= 0 && x < lw) r[(size_t)(x >> 3) * chs + (x & 7)] += qcur[i] * (1.0f - fy) + qprev[i] * fy;
+                }
             }
         }
 #pragma unroll
