@@ -57,6 +57,8 @@ CASES = [
     (1, 256, 46, 62, 4, 4, 4.0, (3, 6)),       # cfg1 feature shape, levels 0 and 3 masked
     (1, 8, 9, 70, 1, 1, 0.5, ()),              # one level, r=1, wide map
     (1, 320, 14, 20, 3, 3, 2.0, ()),           # C > 256: runtime-channel path (Cp 384: 12 bf16 / 24 f32 load steps)
+    (1, 48, 20, 36, 2, 8, 3.0, ()),            # r=8: 17 x 17 window, three interpolation items per thread
+    (2, 128, 18, 40, 3, 5, 2.0, (5,)),         # r=5, C=128, level 0 masked
 ]
 
 
@@ -125,7 +127,8 @@ def test_otf_full_size_agrees_with_volume_path(precision):
     assert rel_max_err(a.cpu().numpy(), ref.cpu().numpy()) < TOL[precision]
 
 
-def test_otf_wide_map_agrees_with_volume_path():
+@pytest.mark.parametrize("radius", [4, 7])
+def test_otf_wide_map_agrees_with_volume_path(radius):
     """bf16 on a wide map (B=4, 128x256: 4,096 16x2 query blocks) takes the 16x4-block kernel
     (csrc/corr_otf.hip kWideBlocks); it must equal the pyramid + lookup within the bf16 tolerance, with
     large and small displacements, and be deterministic."""
@@ -137,10 +140,10 @@ def test_otf_wide_map_agrees_with_volume_path():
     co = torch.stack([xs, ys])[None] + 6 * torch.randn(4, 2, 128, 256, generator=g)
     co[1] += 40.0                                      # one image with a large shift (boxes off the map)
     co = co.to(DEV)
-    otf = rmd.raft_fs.CorrBlock(f1, f2, 4, 4, precision="bf16", method="otf")
+    otf = rmd.raft_fs.CorrBlock(f1, f2, 4, radius, precision="bf16", method="otf")
     a = otf(co)
     b = otf(co)
-    vol = rmd.raft_fs.CorrBlock(f1, f2, 4, 4, precision="fp32")
+    vol = rmd.raft_fs.CorrBlock(f1, f2, 4, radius, precision="fp32")
     ref = vol(co)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
