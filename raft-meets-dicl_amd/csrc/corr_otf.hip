@@ -43,6 +43,16 @@ constexpr int kThreads = 256;                        // prepare kernels
 #ifndef RMD_OTF_NT_X
 #define RMD_OTF_NT_X 512
 #endif
+// wide-map bf16 query block (16 x WQY), workgroup size and occupancy hint (-D knobs for A/B builds)
+#ifndef RMD_OTF_WQY
+#define RMD_OTF_WQY 4
+#endif
+#ifndef RMD_OTF_WNT
+#define RMD_OTF_WNT 512
+#endif
+#ifndef RMD_OTF_WOCC
+#define RMD_OTF_WOCC 2
+#endif
 constexpr long long kWideBlocks = 4096;              // bf16: 16x4 query blocks from this many 16x2 blocks
 constexpr int kMaxTasks = 1024;                      // box segments of the MFMA path (more: per-query VALU)
 // Query block, occupancy and query-fragment placement per compute (-D knobs for A/B builds,
@@ -1046,8 +1056,8 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         constexpr bool XS = false;
         constexpr size_t XN = 1;
         constexpr bool QLK = true;
-        constexpr int NTK = 512;
-        RMD_OTF_R(__bf16, 1, 4, 2)
+        constexpr int NTK = RMD_OTF_WNT;
+        RMD_OTF_R(__bf16, 1, RMD_OTF_WQY, RMD_OTF_WOCC)
     } else if (compute == RMD_BF16) {
         constexpr bool XS = false;
         constexpr size_t XN = 1;
