@@ -9,9 +9,12 @@ input; rmd_input_flow pads the flow target and its validity mask the same way.
   InputSpec       <- input.py:153-190; InputSpec.prepare() = Input.__getitem__ (input.py:208-226)
                      followed by TorchAdapter.__getitem__ (input.py:245-313) on the GPU
 
-Differences: the statistic pad modes (maximum, mean, median, minimum) raise NotImplementedError (no
-config uses them; every cfg pads with zeros); the non-finite-input warnings of TorchAdapter (which
-only mark metadata) are left to the caller.
+prepare(device='cpu') runs the reference's own host path (numpy clip / range map / np.pad, NCHW
+permute) and returns CPU tensors, so the module works on either device as the reference's does.
+
+Differences: on the GPU the statistic pad modes (maximum, mean, median, minimum) raise
+NotImplementedError (no config uses them; every cfg pads with zeros; the host path supports them);
+the non-finite-input warnings of TorchAdapter (which only mark metadata) are left to the caller.
 """
 
 import numpy as np
@@ -112,8 +115,10 @@ class InputSpec:
         img1, img2 (B,C,H',W') float32, flow (B,2,H',W') float32, valid (B,H',W') bool, extents
         ((h1, h2), (w1, w2)) per input.py:133-135, all on the GPU."""
         device = torch.device(device)
+        if device.type == "cpu":
+            return self._prepare_host(img1, img2, flow, valid)
         if device.type != "cuda":
-            raise RuntimeError("rmd: HIP kernels need GPU tensors (no CPU fallback exists)")
+            raise RuntimeError(f"rmd: prepare() runs on 'cuda' (HIP kernels) or 'cpu', got '{device.type}'")
         i1, i2 = _to_gpu(img1, torch.float32, device), _to_gpu(img2, torch.float32, device)
         if i1.dim() != 4 or i1.shape != i2.shape:
             raise ValueError(f"img1/img2 must be equal (B,H,W,C) shapes, got {tuple(i1.shape)} / {tuple(i2.shape)}")
@@ -145,3 +150,45 @@ class InputSpec:
         # input.py:133-135 adds (ph1, ph2) / (pw1, pw2) to the original ((0, h), (0, w)) extents
         extents = ((ph1, h + ph2), (pw1, w + pw2))
         return outs[0], outs[1], fo, vo, extents
+
+    def _prepare_host(self, img1, img2, flow, valid):
+        """device='cpu': the reference's own host path — np.clip + range map (input.py:215-221), np.pad
+        in the padding mode (input.py:79-138; the statistic modes too), NHWC -> NCHW and the flow's
+        nan_to_num / clip to +-FLOW_INF (TorchAdapter, input.py:245-313) — as CPU tensors."""
+        def host(a, dtype):
+            a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+            return np.ascontiguousarray(a, dtype=dtype)
+        i1, i2 = host(img1, np.float32), host(img2, np.float32)
+        if i1.ndim != 4 or i1.shape != i2.shape:
+            raise ValueError(f"img1/img2 must be equal (B,H,W,C) shapes, got {tuple(i1.shape)} / {tuple(i2.shape)}")
+        b, h, w, c = i1.shape
+        if self.padding is not None:
+            hp, wp, (ph1, ph2), (pw1, pw2) = self.padding.extents(h, w)
+        else:
+            hp, wp, ph1, ph2, pw1, pw2 = h, w, 0, 0, 0, 0
+        widths = ((0, 0), (ph1, ph2), (pw1, pw2), (0, 0))
+
+        def pad(a):
+            if self.padding is None or (ph1, ph2, pw1, pw2) == (0, 0, 0, 0):
+                return a
+            mode = self.padding.mode
+            if mode in ("zeros", "ones"):
+                return np.pad(a, widths, mode="constant", constant_values=0.0 if mode == "zeros" else 1.0)
+            np_mode = {"torch.replicate": "edge", "torch.reflect": "reflect", "torch.circular": "wrap"}.get(mode, mode)
+            return np.pad(a, widths, mode=np_mode)
+
+        outs = []
+        for im in (i1, i2):
+            im = (self.range[1] - self.range[0]) * np.clip(im, self.clip[0], self.clip[1]) + self.range[0]
+            outs.append(torch.from_numpy(np.ascontiguousarray(pad(im.astype(np.float32)).transpose(0, 3, 1, 2))))
+        fo = vo = None
+        if flow is not None:
+            fl, va = host(flow, np.float32), host(valid, np.bool_)
+            if fl.shape != (b, h, w, 2) or va.shape != (b, h, w):
+                raise ValueError(f"flow/valid must be (B,H,W,2)/(B,H,W), got {fl.shape} / {va.shape}")
+            fl = np.clip(np.nan_to_num(fl, nan=0.0, posinf=FLOW_INF, neginf=-FLOW_INF), -FLOW_INF, FLOW_INF)
+            fl = np.pad(fl.astype(np.float32), widths, mode="constant")
+            va = np.pad(va, widths[:3], mode="constant")
+            fo = torch.from_numpy(np.ascontiguousarray(fl.transpose(0, 3, 1, 2)))
+            vo = torch.from_numpy(np.ascontiguousarray(va))
+        return outs[0], outs[1], fo, vo, ((ph1, h + ph2), (pw1, w + pw2))

@@ -58,5 +58,23 @@ def test_input_errors_match_reference():
     spec = InputSpec(padding=ModuloPadding("median", [8, 8]))
     with pytest.raises(NotImplementedError):
         spec.prepare(np.zeros((1, 4, 4, 3), np.float32), np.zeros((1, 4, 4, 3), np.float32))
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        InputSpec().prepare(np.zeros((1, 4, 4, 3), np.float32), np.zeros((1, 4, 4, 3), np.float32), device="cpu")
+    with pytest.raises(RuntimeError, match="runs on 'cuda'"):
+        InputSpec().prepare(np.zeros((1, 4, 4, 3), np.float32), np.zeros((1, 4, 4, 3), np.float32), device="meta")
+
+
+def test_input_gpu_and_host_paths_agree():
+    """The same frames through prepare(device='cuda') (HIP kernels) and prepare(device='cpu') (the
+    reference's host numpy path): bitwise equal, the GPU result on the GPU, the host one on the CPU."""
+    from rmd.input import InputSpec, ModuloPadding
+    rng = np.random.default_rng(12)
+    img1, img2 = (rng.uniform(-0.2, 1.2, (2, 37, 53, 3)).astype(np.float32) for _ in range(2))
+    flow = rng.normal(0, 5, (2, 37, 53, 2)).astype(np.float32)
+    flow[0, 0, 0, 0] = np.nan
+    valid = rng.uniform(size=(2, 37, 53)) > 0.3
+    spec = InputSpec(padding=ModuloPadding("reflect", [16, 8], align_hz="center", align_vt="bottom"))
+    g = spec.prepare(img1, img2, flow, valid)
+    h = spec.prepare(img1, img2, flow, valid, device="cpu")
+    assert g[0].is_cuda and not h[0].is_cuda
+    for a, b in zip(g[:4], h[:4]):
+        assert np.array_equal(a.cpu().numpy(), b.numpy())
+    assert g[4] == h[4]
