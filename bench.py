@@ -668,8 +668,9 @@ def live_traffic(args, precision, batch, rank, device=None):
 
 
 def stored_traffic(precision):
-    """Counter bytes of an earlier profiled run (profiles/pmc_r02.json) — only where no live pass ran."""
-    for name in ("pmc_r02.json", "pmc_r01.json"):
+    """Counter bytes of an earlier profiled run (profiles/pmc_r04.json, tiles layout; older files after it)
+    — only where no live pass ran."""
+    for name in ("pmc_r04.json", "pmc_r02.json", "pmc_r01.json"):
         path = os.path.join(ROOT, "profiles", name)
         if os.path.exists(path):
             try:
