@@ -82,8 +82,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--skip-4k", action="store_true")
+    ap.add_argument("--cfg2-off", action="store_true", help="only the 4K leg")
     a = ap.parse_args()
     out = {}
+    if a.cfg2_off:
+        out["highres_4k"] = highres(a.precision, a.reps)
+        print(json.dumps(out, indent=1))
+        return
     b, c, h, w, iters = 8, 256, 55, 128, 12
     f1, f2, coords = inputs(b, c, h, w, iters)
     g = torch.Generator(device="cpu").manual_seed(5)
