@@ -100,6 +100,10 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_ILV
 #define RMD_OTF_ILV 1
 #endif
+// backward ablation for A/B timing only (wrong results): 1 = the dP atomic adds are skipped
+#ifndef RMD_OTF_BWD_ABL
+#define RMD_OTF_BWD_ABL 0
+#endif
 // pad slots per query patch in LDS (odd patch stride): 1, or 4 = one per lane group (put's pad writes of
 // the 4 lane groups of a query go to distinct addresses)
 #ifndef RMD_OTF_PADS
@@ -884,7 +888,8 @@ otf_backward_kernel(BwdArgs a) {
                         for (int v = 0; v < 16; ++v) {
                             const int col = mt * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
                             const int tx = cx + col;
-                            if (col < ncols && tx <= ext.y && ch < g.C)
+                            if (col < ncols && tx <= ext.y && ch < g.C &&
+                                (RMD_OTF_BWD_ABL == 0 || accp[t][v] == 1.2345e30f))      // ablation: no adds
                                 atomicAdd(drow + (size_t)tx * g.C + ch, (double)accp[t][v]);
                         }
                     }
