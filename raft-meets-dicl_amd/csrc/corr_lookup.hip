@@ -473,6 +473,9 @@ __device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ py
 }
 
 // grid: (slot blocks of 64, batch, level + levels * part) — one lane per (query slot, level, row part)
+#ifndef RMD_LOOKUP_ZORD
+#define RMD_LOOKUP_ZORD 0
+#endif
 #ifndef RMD_LOOKUP_WPE8
 #define RMD_LOOKUP_WPE8 0
 #endif
@@ -486,10 +489,20 @@ __global__ void __launch_bounds__(kThreads) RMD_LOOKUP_ATTR
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
     const int N = g.height * g.width;
+#if RMD_LOOKUP_ZORD
+    // A/B: the 3 row parts of a slot block 8 blocks apart (one XCD under round-robin dispatch), one
+    // level per z (ZORD 2: level 0 last)
+    const int grp = (int)blockIdx.x / 24, rem = (int)blockIdx.x - grp * 24;
+    const int part = rem >> 3;
+    const int s = (grp * 8 + (rem & 7)) * kThreads + threadIdx.x;
+    if ((grp * 8 + (rem & 7)) * kThreads >= g.slots) return;
+    const int L = RMD_LOOKUP_ZORD == 2 ? g.levels - 1 - (int)blockIdx.z : (int)blockIdx.z;
+#else
     const int s = blockIdx.x * kThreads + threadIdx.x;
-    const int b = blockIdx.y;
     const int L = (int)blockIdx.z % g.levels;
     const int part = (int)blockIdx.z / g.levels;
+#endif
+    const int b = blockIdx.y;
     bool active;
     int p, slot;
     if constexpr (LAY == RMD_LAYOUT_TILES) {
@@ -537,7 +550,11 @@ template <typename T, int LAY>
 int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coords, int radius, unsigned zmask,
                   float* out, hipStream_t st) {
     const PyrGeom g = make_geom(d);
+#if RMD_LOOKUP_ZORD
+    const dim3 grid(((g.slots + kThreads - 1) / kThreads + 7) / 8 * 24, d.batch, d.levels);
+#else
     const dim3 grid((g.slots + kThreads - 1) / kThreads, d.batch, d.levels * 3);
+#endif
     const T* p = reinterpret_cast<const T*>(pyr);
     // buffer loads need every per-image level slab below 2^31 bytes (kOOB must lie past it); the
     // pointer path stays for larger pyramids (-DRMD_LOOKUP_BUF=0 forces it for A/B builds)

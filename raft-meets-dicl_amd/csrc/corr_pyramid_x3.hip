@@ -439,6 +439,157 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
     }
 }
 
+// ---- one wave per SIMD, QT query tiles per pass --------------------------------------------------
+// Four waves per workgroup (one per SIMD, up to 512 registers each), no barriers after the A staging:
+// each wave sweeps passes of QT query tiles (tiles w QT + 4 QT i + {0..QT-1}) against the whole
+// 128-target block, so every A fragment read from LDS feeds 3 QT MFMAs (3 with one query tile) and the
+// MFMA stream of a pass is 12 QT per k-step.  B fragments of the QT tiles stream through a DR-k-step
+// register ring as in corr_pyramid_x3.
+#ifndef RMD_X3_QT
+#define RMD_X3_QT 2
+#endif
+#ifndef RMD_X3_DR
+#define RMD_X3_DR 4
+#endif
+
+template <int QT, int DR, int S>
+__device__ __forceinline__ void v2_ksteps(f32x16 (&acc)[QT][4], bf16x8 (&acur)[8], bf16x8 (&anext)[8],
+                                          bf16x8 (&rh)[DR][QT], bf16x8 (&rl)[DR][QT], const unsigned char* smem,
+                                          unsigned b0, unsigned b1, const __bf16* const (&cur)[QT],
+                                          const __bf16* const (&nxt)[QT], size_t lo_off) {
+    if constexpr (S < 16) {
+        if constexpr (S + 1 < 16) read_a<S + 1>(anext, smem, b0, b1);
+        {   // B fragments of k-step S + DR - 1 (this pass) or of the next pass's k-step S + DR - 1 - 16
+            constexpr int T = S + DR - 1, slot = T % DR;
+#pragma unroll
+            for (int qi = 0; qi < QT; ++qi) {
+                const __bf16* p = (T < 16 ? cur[qi] : nxt[qi]) + 512 * (T & 15);
+                rh[slot][qi] = *reinterpret_cast<const bf16x8*>(p);
+                rl[slot][qi] = *reinterpret_cast<const bf16x8*>(p + lo_off);
+            }
+        }
+        const f32x16 zero = {};
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+            for (int qi = 0; qi < QT; ++qi) {
+                const bf16x8 bh = rh[S % DR][qi], bl = rl[S % DR][qi];
+                f32x16 c = S == 0 ? zero : acc[qi][ti];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti + 1], bh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bl, c, 0, 0, 0);
+                acc[qi][ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bh, c, 0, 0, 0);
+            }
+        if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2 * QT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 12 * QT, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        v2_ksteps<QT, DR, S + 1>(acc, anext, acur, rh, rl, smem, b0, b1, cur, nxt, lo_off);
+    }
+}
+
+template <int QT, int DR, int ABL = 0>
+__global__ void __launch_bounds__(256, 1)
+corr_pyramid_x3v2(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
+                  const __bf16* __restrict__ bLo, PyrGeom g, int units, float* __restrict__ pyr) {
+    constexpr int WAVES = 4;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int H = g.height, W = g.width, N = H * W;
+    const int ncb = (W + kBlockCols - 1) / kBlockCols;
+    const int nblk = ((H + kBlockRows - 1) / kBlockRows) * ncb;
+    const int nqt = (N + 31) >> 5;
+    const int u = xcd_block(blockIdx.x, gridDim.x);
+    if (u >= units) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 31, h = lane >> 5;
+    const int b = u / nblk, tb = u - b * nblk;
+    const int rb = tb / ncb, cb = tb - rb * ncb;
+    const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
+
+    // ---- A block (hi and lo) -> LDS: 32 pieces per thread, in two halves of 16 loads in flight ----
+    const size_t abase = (size_t)b * N * 256;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint4 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int id = tid + (half * 16 + i) * 64 * WAVES;
+            const int row = id >> 6, c = id & 63;
+            const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
+            const __bf16* src = c < 32 ? aHi : aLo;
+            v[i] = make_uint4(0, 0, 0, 0);
+            if (ty < H && tx < W) v[i] = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int id = tid + (half * 16 + i) * 64 * WAVES;
+            const int row = id >> 6, c = id & 63;
+            *reinterpret_cast<uint4*>(smem + (size_t)lds_row(row >> 4, row & 15) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v[i];
+        }
+    }
+    __syncthreads();
+
+    Lvl L[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const int span = kBlockRows >> l, nch = l == 0 ? 2 : 1;
+        const int y0 = rb * span, xc0 = cb * nch;
+        const bool lv = l < g.levels;
+        const int cw = g.tw[l];
+        const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 4u : 0u;
+        const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
+        float* bp = pyr + base;
+        const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
+        const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
+        L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
+                                                      (int)__builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs),
+                                                      0x00020000);
+        L[l].rs = __builtin_amdgcn_readfirstlane(rs);
+        L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
+        L[l].rows = __builtin_amdgcn_readfirstlane(rows);
+        L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+    }
+
+    unsigned b0 = (unsigned)j * kRow + 16u * h, b1 = b0 + 64u * kRow;
+    asm volatile("" : "+v"(b0), "+v"(b1));
+    const __bf16* bbase = bHi + ((size_t)b * nqt * 1024 + lane) * 8;
+    const size_t lo_off = (size_t)(bLo - bHi);
+    constexpr int STEP = WAVES * QT;
+    // passes of this wave: tiles t0 + {0..QT-1} with t0 = w QT + STEP i; a tile past the map recomputes
+    // tile nqt - 1 (identical values rewritten)
+    const int npass = (nqt - w * QT + STEP - 1) / STEP;
+    bf16x8 rh[DR][QT], rl[DR][QT];
+    if (npass > 0) {
+#pragma unroll
+        for (int qi = 0; qi < QT; ++qi) {
+            const __bf16* p = bbase + (size_t)min(w * QT + qi, nqt - 1) * 8192;
+#pragma unroll
+            for (int s = 0; s < DR - 1; ++s) {
+                rh[s][qi] = *reinterpret_cast<const bf16x8*>(p + 512 * s);
+                rl[s][qi] = *reinterpret_cast<const bf16x8*>(p + 512 * s + lo_off);
+            }
+        }
+    }
+    vmcnt_pad_n<kEpiStores * QT>(pyr);
+    for (int i = 0; i < npass; ++i) {
+        const int t0 = w * QT + STEP * i;
+        const __bf16* cur[QT];
+        const __bf16* nxt[QT];
+#pragma unroll
+        for (int qi = 0; qi < QT; ++qi) {
+            cur[qi] = bbase + (size_t)min(t0 + qi, nqt - 1) * 8192;
+            nxt[qi] = bbase + (size_t)min(t0 + STEP + qi, nqt - 1) * 8192;
+        }
+        f32x16 acc[QT][4];
+        bf16x8 a0[8], a1[8];
+        read_a<0>(a0, smem, b0, b1);
+        v2_ksteps<QT, DR, 0>(acc, a0, a1, rh, rl, smem, b0, b1, cur, nxt, lo_off);
+#pragma unroll
+        for (int qi = 0; qi < QT; ++qi) epilogue(acc[qi], L, min((t0 + qi) * 32 + j, N - 1), h);
+    }
+}
+
 }  // namespace
 
 bool eligible(const rmd_pyramid_desc& d, int C) {
@@ -475,6 +626,16 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const __bf16* bHi = aLo + (size_t)d.batch * N * 256;
     const __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
     const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
+#if RMD_X3_V2
+    {
+        const int units = nblk * d.batch;
+        const int lds = kBlockRows * kBlockCols * kRow;
+        auto kern = corr_pyramid_x3v2<RMD_X3_QT, RMD_X3_DR, RMD_X3_ABL>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        kern<<<units, 256, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<float*>(pyr));
+        return check_launch("rmd_corr_pyramid/gemm-x3v2");
+    }
+#endif
     // schedule (see corr_pyramid_x3): quarters Q in {1, 2, 4, 8} minimising slots x rounds per unit,
     // slots = ceil(B nblk Q / CUs) (one 137-KB-LDS workgroup per CU), rounds = ceil(nqt / Q / 8); a
     // unit re-stages A, charged as 0.3 round.  Q = 1 with one workgroup per unit is the plain launch

@@ -53,6 +53,24 @@ def test_otf_training_channel_limit():
     assert config.choose_method("otf", 8, 270, 480, 4, "bf16", False, 1 << 30, channels=512) == "otf"
 
 
+def test_cpu_otf_block_trains_above_256_channels():
+    # the C <= 256 limit is the HIP backward's: a CPU block with C = 320 and method='otf' trains
+    # through the ATen kernels
+    import torch
+
+    import rmd
+    g = torch.Generator().manual_seed(0)
+    f1 = torch.randn(1, 320, 6, 8, generator=g, requires_grad=True)
+    f2 = torch.randn(1, 320, 6, 8, generator=g, requires_grad=True)
+    cb = rmd.raft.CorrBlock(f1, f2, 2, 2, precision="fp32", method="otf")
+    assert cb.method == "otf"
+    ys, xs = torch.meshgrid(torch.arange(6.0), torch.arange(8.0), indexing="ij")
+    coords = torch.stack([xs, ys])[None] + 0.3
+    cb(coords).square().sum().backward()
+    assert f1.grad is not None and f2.grad is not None
+    assert torch.isfinite(f1.grad).all() and float(f2.grad.abs().sum()) > 0
+
+
 def test_configure_restore():
     prev = config.configure({"corr-precision": "bf16"})
     try:
