@@ -550,7 +550,21 @@ def init_distributed(args):
         else:
             dist.init_process_group(args.backend, timeout=tmo)
         assert dist.get_world_size() == world
+        global _HOST_GROUP
+        # a gloo group for the closing barrier: ranks waiting there for rank 0's cpu_baseline block in a
+        # socket read instead of spin-waiting on a RCCL stream (the CPU baseline is timed on an
+        # otherwise idle host)
+        _HOST_GROUP = dist.new_group(backend="gloo", timeout=tmo) if args.backend != "gloo" else None
     return world, rank, device
+
+
+_HOST_GROUP = None
+
+
+def host_barrier():
+    """Barrier whose waiters sleep in a gloo socket read (not a spinning RCCL stream sync)."""
+    import torch.distributed as dist
+    dist.barrier(group=_HOST_GROUP) if _HOST_GROUP is not None else dist.barrier()
 
 
 HBM_COPY_GBS = 6290.0          # measured float4 copy rate (MI355X_MICROARCH.md chip table)
@@ -657,14 +671,70 @@ def live_traffic(args, precision, batch, rank, device=None):
                 vals.setdefault(key, []).append(float(row["Counter_Value"]) * 1024.0)
         for k, v in vals.items():
             per.setdefault(k, {})[counter] = (sum(v) / len(v), len(v))
+    mfma = mfma_busy_pass(args, precision, batch, rank, device, d, exe)
     shutil.rmtree(d, ignore_errors=True)
     res = {}
     for k, c in per.items():
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             res[k] = {"read": 2.0 * c["FETCH_SIZE"][0], "write": c["WRITE_SIZE"][0],
                       "total": 2.0 * c["FETCH_SIZE"][0] + c["WRITE_SIZE"][0], "dispatches": c["FETCH_SIZE"][1]}
+    if mfma:
+        res.setdefault("gemm", {})["mfma_counters"] = mfma
     return res, ("live: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (KiB -> B, gfx950 correction), this run, tools/pmc_probe.py "
                  f"on rank {rank}'s GPU")
+
+
+def mfma_busy_pass(args, precision, batch, rank, device, d, exe):
+    """Counter-evidenced MFMA utilisation of the GEMM (north_star: 'MFMA utilisation for the correlation
+    GEMM'): one rocprofv3 pass of SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE with the kernel trace over
+    tools/pmc_probe.py.  MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe cycles summed over
+    every SIMD (32 per v_mfma_f32_32x32x16_bf16); GRBM_GUI_ACTIVE the busy cycles summed over the 8 XCDs.
+      mfma_busy = MFMA cycles / (SIMDs x GRBM_GUI_ACTIVE / 8)   (fraction of the chip's matrix-pipe cycles)
+      clock     = GRBM_GUI_ACTIVE / 8 / kernel duration          (the effective clock the launch ran at)
+    The first dispatch (cold clocks) is dropped."""
+    import csv
+    import glob
+    import subprocess
+    out = os.path.join(d, "mfma")
+    cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "--kernel-trace",
+           "--output-format", "csv", "-d", out, "-o", "run",
+           "--", sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), "--precision", precision,
+           "--batch", str(batch), "--height", str(args.height), "--width", str(args.width),
+           "--channels", str(args.channels), "--iters", str(args.iters)]
+    progress(rank, f"live PMC pass SQ_VALU_MFMA_BUSY_CYCLES ({precision})")
+    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, cwd=d, env=child_env(device))
+    cfiles = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+    tfiles = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not cfiles:
+        return {"error": f"rocprofv3 MFMA pass failed (rc {r.returncode}): {r.stderr.decode()[-200:]}"}
+    vals, durs = {}, {}
+    for row in csv.DictReader(open(cfiles[0])):
+        if "corr_pyramid_" in row["Kernel_Name"]:
+            key = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            vals.setdefault(key, {}).setdefault(row["Counter_Name"], 0.0)
+            vals[key][row["Counter_Name"]] += float(row["Counter_Value"])
+    for f in tfiles:
+        for row in csv.DictReader(open(f)):
+            if "corr_pyramid_" in row["Kernel_Name"]:
+                key = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                durs[key] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
+    keys = sorted((k for k in vals if "SQ_VALU_MFMA_BUSY_CYCLES" in vals[k] and "GRBM_GUI_ACTIVE" in vals[k]), key=int)
+    if len(keys) > 1:
+        keys = keys[1:]
+    if not keys:
+        return {"error": "no GEMM dispatch in the MFMA pass"}
+    simds = 4 * torch.cuda.get_device_properties(device).multi_processor_count
+    busy = sum(vals[k]["SQ_VALU_MFMA_BUSY_CYCLES"] for k in keys) / len(keys)
+    grbm = sum(vals[k]["GRBM_GUI_ACTIVE"] for k in keys) / len(keys)
+    res = {"mfma_busy": busy / (simds * grbm / 8), "SQ_VALU_MFMA_BUSY_CYCLES": busy, "GRBM_GUI_ACTIVE": grbm,
+           "simds": simds, "dispatches": len(keys),
+           "source": "live: rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace, this run, "
+                     f"tools/pmc_probe.py on rank {rank}'s GPU"}
+    dk = [durs[k] for k in keys if k in durs]
+    if dk:
+        res["profiled_duration_ms"] = sum(dk) / len(dk) * 1e3
+        res["clock_ghz"] = grbm / 8 / (sum(dk) / len(dk)) / 1e9
+    return res
 
 
 def stored_traffic(precision):
@@ -730,6 +800,10 @@ def rooflines(args, precision, B, h8, w8, gemm_ms, look_ms, traffic, traffic_not
                  "mfma_ceiling_note": (f"algorithmic bytes at the {HBM_COPY_GBS / 1e3:.2f} TB/s measured copy rate "
                                        f"(spec {HBM_PEAK_GBS / 1e3:.0f} TB/s) cap the fused-pyramid GEMM's MFMA fraction"),
                  "algorithmic_flop_per_launch": gemm_flop}
+    mc = traffic.get("gemm", {}).get("mfma_counters")
+    if mc:
+        roof_gemm["mfma_busy"] = mc.get("mfma_busy")
+        roof_gemm["mfma_counters"] = mc
     roof_look = {"kernel": "corr_lookup_kernel", "bound": "hbm", "achieved": look_gbs, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": look_gbs / HBM_PEAK_GBS, "traffic": lt,
                  "traffic_read": tr("lookup", "read"), "traffic_write": tr("lookup", "write"),
@@ -847,10 +921,12 @@ def main():
             res["cpu_baseline"] = cpu_baseline(args)
             if world > 1:
                 res["cpu_baseline"]["note"] = (f"rank 0 of {world}, timed after every GPU leg while the other ranks "
-                                               f"wait at a barrier")
+                                               f"sleep in a gloo barrier (no spin-waiting HIP sync on the host)")
         print(json.dumps(res), flush=True)
     if world > 1:
-        torch.distributed.barrier()
+        if not args.dry_run:
+            torch.cuda.synchronize(device)
+        host_barrier()
         torch.distributed.destroy_process_group()
 
 

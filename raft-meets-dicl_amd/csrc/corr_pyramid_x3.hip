@@ -27,6 +27,10 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+#ifndef RMD_X3_S16TEST
+#define RMD_X3_S16TEST 0
+#endif
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 typedef __attribute__((ext_vector_type(2))) int i32x2;
 
@@ -48,6 +52,7 @@ __device__ __forceinline__ __bf16 lo_part(float v) { return (__bf16)(v - (float)
 // hi and lo tiles staged in LDS, one 16-B chunk per lane-store on the write side.
 constexpr int kPx = 128, kStride = 256 * 2 + 16;
 
+template <bool S16>
 __global__ void __launch_bounds__(512)
 prep_split(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* __restrict__ aHi,
            __bf16* __restrict__ aLo, __bf16* __restrict__ bHi, __bf16* __restrict__ bLo, int C, int N, int nqt,
@@ -104,7 +109,12 @@ prep_split(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* _
     for (int it = 0; it < 8; ++it) {
         const int k = it * 512 + t;                  // 16-B output chunk of the tile's 64 KiB block
         int px, c0;
-        if (which) {
+        if (which && S16) {
+            // 16x16x32 B fragments: 16-query tile t16 = k >> 9, k-step (32 channels) st, lane n + 16 g
+            const int L = k & 63, st = (k >> 6) & 7;
+            px = (k >> 9) * 16 + (L & 15);
+            c0 = 32 * st + 8 * (L >> 4);
+        } else if (which) {
             const int L = k & 63, st = (k >> 6) & 15;
             px = (k >> 10) * 32 + (L & 31);
             c0 = 16 * st + 8 * (L >> 5);
@@ -114,7 +124,14 @@ prep_split(const float* __restrict__ f1, const float* __restrict__ f2, __bf16* _
         }
         const bf16x8 hi = *reinterpret_cast<const bf16x8*>(tHi + (size_t)px * kStride + c0 * 2);
         const bf16x8 lo = *reinterpret_cast<const bf16x8*>(tLo + (size_t)px * kStride + c0 * 2);
-        if (which) {
+        if (which && S16) {
+            const int t16 = blockIdx.x * 8 + (k >> 9);
+            if (t16 < 2 * nqt) {
+                const size_t o = (((size_t)b * 2 * nqt + t16) * 512 + (k & 511)) * 8;
+                *reinterpret_cast<bf16x8*>(bHi + o) = hi;
+                *reinterpret_cast<bf16x8*>(bLo + o) = lo;
+            }
+        } else if (which) {
             const int qt = blockIdx.x * 4 + (k >> 10);
             if (qt < nqt) {
                 const size_t o = (((size_t)b * nqt + qt) * 1024 + (k & 1023)) * 8;
@@ -159,6 +176,18 @@ constexpr int AUX_NT = 2;     // non-temporal stores: the pyramid is re-read a w
 
 // Epilogue of one 32-query tile: acc[ti] (ti = 2 rg + cg) holds, for lane (j, h), the targets
 // (row 4 rg + k, col 8 cg + 4 h + e) at acc[ti][4k + e].
+#ifndef RMD_X3_S24TEST
+#define RMD_X3_S24TEST 0
+#endif
+typedef __attribute__((ext_vector_type(3))) int i32x3;
+// 4 floats -> 3 words of their top 24 bits (rounded), for the 24-bit storage timing variant
+__device__ __forceinline__ i32x3 pack24(float a, float b, float c, float d) {
+    const unsigned v0 = __float_as_uint(a) + 0x80u, v1 = __float_as_uint(b) + 0x80u;
+    const unsigned v2 = __float_as_uint(c) + 0x80u, v3 = __float_as_uint(d) + 0x80u;
+    return i32x3{(int)__builtin_amdgcn_perm(v1, v0, 0x05030201u), (int)__builtin_amdgcn_perm(v2, v1, 0x06050302u),
+                 (int)__builtin_amdgcn_perm(v3, v2, 0x07060503u)};
+}
+
 __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[4], int q, int h) {
     const unsigned qo[4] = {(unsigned)q * 32u + 16u * h, (unsigned)q * 32u + 16u * h, (unsigned)q * 16u + 8u * h,
                             (unsigned)q * 8u + 4u * h};
@@ -167,10 +196,16 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
     for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+#if RMD_X3_S24TEST
+            const i32x3 d3 = pack24(acc[ti][4 * k + 0], acc[ti][4 * k + 1], acc[ti][4 * k + 2], acc[ti][4 * k + 3]);
+            __builtin_amdgcn_raw_buffer_store_b96(d3, L[0].rsrc, (int)((qo[0] + soff(L[0], 4 * (ti >> 1) + k, ti & 1)) / 4u * 3u),
+                                                  0, AUX_NT);
+#else
             const i32x4 d = {__float_as_int(acc[ti][4 * k + 0]), __float_as_int(acc[ti][4 * k + 1]),
                              __float_as_int(acc[ti][4 * k + 2]), __float_as_int(acc[ti][4 * k + 3])};
             __builtin_amdgcn_raw_buffer_store_b128(d, L[0].rsrc, (int)(qo[0] + soff(L[0], 4 * (ti >> 1) + k, ti & 1)),
                                                    0, AUX_NT);
+#endif
         }
     // level 1: tile rows (2m, 2m+1) -> level-1 row 2rg + m; lane pair u -> block col 4cg + 2h + u
     float s2[2][2];      // level-2 sums [rg][cg] (16 level-0 values each)
@@ -196,9 +231,14 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
             float x0 = p[0][0], x1 = p[0][1], y0 = p[1][0], y1 = p[1][1];
             swapf(x0, y0);
             swapf(x1, y1);
+#if RMD_X3_S24TEST
+            __builtin_amdgcn_raw_buffer_store_b96(pack24(0.25f * x0, 0.25f * x1, 0.25f * y0, 0.25f * y1), L[1].rsrc,
+                                                  (int)((qo[1] + soff(L[1], 2 * rg + m, 0)) / 4u * 3u), 0, AUX_NT);
+#else
             const i32x4 d = {__float_as_int(0.25f * x0), __float_as_int(0.25f * x1), __float_as_int(0.25f * y0),
                              __float_as_int(0.25f * y1)};
             __builtin_amdgcn_raw_buffer_store_b128(d, L[1].rsrc, (int)(qo[1] + soff(L[1], 2 * rg + m, 0)), 0, AUX_NT);
+#endif
         }
     }
     // level 2: row rg, lane holds col h (cg 0) and 2 + h (cg 1); after the swap lower = {0,1}, upper = {2,3}
@@ -266,14 +306,30 @@ __device__ __forceinline__ void ksteps(f32x16 (&acc)[4], bf16x8 (&acur)[8], bf16
 #pragma unroll
         for (int ti = 0; ti < 4; ++ti) {
             f32x16 c = S == 0 ? zero : acc[ti];
+#if RMD_X3_S16TEST
+            // timing only (wrong results): each 32x32x16 product as two 16x16x32 MFMAs of the same cycles
+            typedef __attribute__((ext_vector_type(4))) float f32x4;
+            f32x4 p0 = __builtin_shufflevector(c, c, 0, 1, 2, 3), p1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
+            f32x4 p2 = __builtin_shufflevector(c, c, 8, 9, 10, 11), p3 = __builtin_shufflevector(c, c, 12, 13, 14, 15);
+            p0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti + 1], bh, p0, 0, 0, 0);
+            p1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti + 1], bh, p1, 0, 0, 0);
+            p2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti], bl, p2, 0, 0, 0);
+            p3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti], bl, p3, 0, 0, 0);
+            p0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti], bh, p0, 0, 0, 0);
+            p3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * ti], bh, p3, 0, 0, 0);
+            const f32x8 lo8 = __builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7);
+            const f32x8 hi8 = __builtin_shufflevector(p2, p3, 0, 1, 2, 3, 4, 5, 6, 7);
+            acc[ti] = __builtin_shufflevector(lo8, hi8, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#else
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti + 1], bh, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bl, c, 0, 0, 0);
             acc[ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bh, c, 0, 0, 0);
+#endif
         }
         // order inside the region: k-step S+1's 8 LDS reads and the 2 ring loads first, then 12 MFMAs
         if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, RMD_X3_S16TEST ? 24 : 12, 0);
         __builtin_amdgcn_sched_barrier(0);      // one scheduling region per k-step
         ksteps<S + 1>(acc, anext, acur, rh, rl, smem, b0, b1, curH, curL, nxtH, nxtL);
     }
@@ -439,93 +495,163 @@ corr_pyramid_x3(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, 
     }
 }
 
-// ---- one wave per SIMD, QT query tiles per pass --------------------------------------------------
-// Four waves per workgroup (one per SIMD, up to 512 registers each), no barriers after the A staging:
-// each wave sweeps passes of QT query tiles (tiles w QT + 4 QT i + {0..QT-1}) against the whole
-// 128-target block, so every A fragment read from LDS feeds 3 QT MFMAs (3 with one query tile) and the
-// MFMA stream of a pass is 12 QT per k-step.  B fragments of the QT tiles stream through a DR-k-step
-// register ring as in corr_pyramid_x3.
-#ifndef RMD_X3_QT
-#define RMD_X3_QT 2
-#endif
-#ifndef RMD_X3_DR
-#define RMD_X3_DR 4
-#endif
 
-template <int QT, int DR, int S>
-__device__ __forceinline__ void v2_ksteps(f32x16 (&acc)[QT][4], bf16x8 (&acur)[8], bf16x8 (&anext)[8],
-                                          bf16x8 (&rh)[DR][QT], bf16x8 (&rl)[DR][QT], const unsigned char* smem,
-                                          unsigned b0, unsigned b1, const __bf16* const (&cur)[QT],
-                                          const __bf16* const (&nxt)[QT], size_t lo_off) {
-    if constexpr (S < 16) {
-        if constexpr (S + 1 < 16) read_a<S + 1>(anext, smem, b0, b1);
-        {   // B fragments of k-step S + DR - 1 (this pass) or of the next pass's k-step S + DR - 1 - 16
-            constexpr int T = S + DR - 1, slot = T % DR;
+// ---- 16x16x32 form (the product since round 5) -------------------------------------------------
+// The same 8 x 16 target block, ping-pong phases and B ring, with v_mfma_f32_16x16x32_bf16 tiles:
+// a wave's 32-query tile is 2 N-tiles of 16 queries against 8 M-tiles of 16 targets (M-tile mt = 2 rp
+// + ch: rows 2rp, 2rp+1 x cols 8ch..8ch+7 of the block), 8 k-steps of 32 channels, each k-step in two
+// halves of 4 M-tiles (8 A fragments double-buffered, 24 MFMAs per half).  On random operands the chip
+// holds a higher clock under this shape than under 32x32x16 at the same MFMA cycles
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7; profiles/x3_ab_r05.json: the kernel is power-bound,
+// its cycles do not change when its stores are dropped but its clock does).
+//
+// A in LDS, k-major: the 16-B piece of (part p = hi/lo, channel chunk cc = 0..31, LDS row r) sits at
+// ((p * 32 + cc) * 128 + r) * 16, row r = 16 mt + 8 (row in pair) + col in half.  A fragment read
+// (lane n + 16 g: row 16 mt + n, chunk 4 s + g) gives every 16-lane ds_read_b128 group 16 distinct rows
+// = 16 distinct 16-B bank slots (no padding, 128 KiB).
+#ifndef RMD_X3_SHAPE
+#define RMD_X3_SHAPE 16
+#endif
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+constexpr int kLds16 = 2 * 32 * 128 * 16;
+constexpr int kDR16 = 4;                     // B ring depth (k-steps of 32 channels; divides 8)
+constexpr int kEpiStores16 = 30;             // buffer stores of one epilogue16 (16 + 8 + 4 + 2)
+
+__device__ __forceinline__ int s16_row(int y, int x) { return (((y >> 1) * 2 + (x >> 3)) << 4) + ((y & 1) << 3) + (x & 7); }
+
+// A fragments of half-step (k-step S, M-tiles 4M..4M+3): hi in [2i], lo in [2i+1]
+template <int S, int M>
+__device__ __forceinline__ void read_a16(bf16x8 (&a)[8], const unsigned char* smem, unsigned bhi, unsigned blo) {
 #pragma unroll
-            for (int qi = 0; qi < QT; ++qi) {
-                const __bf16* p = (T < 16 ? cur[qi] : nxt[qi]) + 512 * (T & 15);
-                rh[slot][qi] = *reinterpret_cast<const bf16x8*>(p);
-                rl[slot][qi] = *reinterpret_cast<const bf16x8*>(p + lo_off);
-            }
-        }
-        const f32x16 zero = {};
-#pragma unroll
-        for (int ti = 0; ti < 4; ++ti)
-#pragma unroll
-            for (int qi = 0; qi < QT; ++qi) {
-                const bf16x8 bh = rh[S % DR][qi], bl = rl[S % DR][qi];
-                f32x16 c = S == 0 ? zero : acc[qi][ti];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti + 1], bh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bl, c, 0, 0, 0);
-                acc[qi][ti] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[2 * ti], bh, c, 0, 0, 0);
-            }
-        if constexpr (S + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 2 * QT, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 12 * QT, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        v2_ksteps<QT, DR, S + 1>(acc, anext, acur, rh, rl, smem, b0, b1, cur, nxt, lo_off);
+    for (int i = 0; i < 4; ++i) {
+        const unsigned off = (unsigned)(S * 8192 + (4 * M + i) * 256);
+        a[2 * i] = *reinterpret_cast<const bf16x8*>(smem + bhi + off);
+        a[2 * i + 1] = *reinterpret_cast<const bf16x8*>(smem + blo + off);
     }
 }
 
-template <int QT, int DR, int ABL = 0>
-__global__ void __launch_bounds__(256, 1)
-corr_pyramid_x3v2(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
-                  const __bf16* __restrict__ bLo, PyrGeom g, int units, float* __restrict__ pyr) {
-    constexpr int WAVES = 4;
+template <int HS>      // half-step HS = 2 S + M
+__device__ __forceinline__ void ksteps16(f32x4 (&acc)[8][2], bf16x8 (&acur)[8], bf16x8 (&anext)[8],
+                                         bf16x8 (&rh)[kDR16][2], bf16x8 (&rl)[kDR16][2], const unsigned char* smem,
+                                         unsigned bhi, unsigned blo, const __bf16* cur, const __bf16* nxt,
+                                         size_t lo_off) {
+    if constexpr (HS < 16) {
+        constexpr int S = HS >> 1, M = HS & 1;
+        constexpr int SN = (HS + 1) / 2, MN = (HS + 1) % 2;
+        if constexpr (HS + 1 < 16) read_a16<SN, MN>(anext, smem, bhi, blo);
+        {   // N-tile M's B fragments of k-step S + kDR16 - 1 (this tile) or of the next tile's
+            constexpr int T = S + kDR16 - 1, slot = T % kDR16;
+            const __bf16* p = (T < 8 ? cur : nxt) + M * 4096 + 512 * (T & 7);
+            rh[slot][M] = *reinterpret_cast<const bf16x8*>(p);
+            rl[slot][M] = *reinterpret_cast<const bf16x8*>(p + lo_off);
+        }
+        const f32x4 zero = {};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bf16x8 bh = rh[S % kDR16][u], bl = rl[S % kDR16][u];
+                f32x4 c = S == 0 ? zero : acc[4 * M + i][u];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * i + 1], bh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * i], bl, c, 0, 0, 0);
+                acc[4 * M + i][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(acur[2 * i], bh, c, 0, 0, 0);
+            }
+        if constexpr (HS + 1 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        ksteps16<HS + 1>(acc, anext, acur, rh, rl, smem, bhi, blo, cur, nxt, lo_off);
+    }
+}
+
+// Epilogue of one 32-query tile in the 16x16 layout: acc[mt][u][e] is, for lane (n, g) and query
+// 16 u + n, the target (row 2 rp + (g >> 1), col 8 ch + 4 (g & 1) + e) with mt = 2 rp + ch.
+__device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (&L)[4], int qt, int N, int n, int g) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const unsigned q = (unsigned)min(qt * 32 + 16 * u + n, N - 1);
+        // level 0: 1 x 8 fp32 chunks (32 B per query); lanes g = 2 r', 2 r' + 1 write row r' bytes 0-15 / 16-31
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+            const i32x4 d = {__float_as_int(acc[mt][u][0]), __float_as_int(acc[mt][u][1]), __float_as_int(acc[mt][u][2]),
+                             __float_as_int(acc[mt][u][3])};
+            __builtin_amdgcn_raw_buffer_store_b128(
+                d, L[0].rsrc, (int)(q * 32u + 16u * (g & 1) + soff(L[0], 2 * (mt >> 1) + (g >> 1), mt & 1)), 0, AUX_NT);
+        }
+        // level 1: horizontal pairs in-lane, vertical pairs across the lane halves (ch 0 lands in the lower,
+        // ch 1 in the upper half): lane g then holds level-1 cols 2g, 2g+1 of level-1 row rp
+        float t2[2];
+#pragma unroll
+        for (int rp = 0; rp < 4; ++rp) {
+            const f32x4& a = acc[2 * rp][u];
+            const f32x4& c = acc[2 * rp + 1][u];
+            float x0 = a[0] + a[1], x1 = a[2] + a[3], y0 = c[0] + c[1], y1 = c[2] + c[3];
+            swapf(x0, y0);
+            swapf(x1, y1);
+            const float s0 = x0 + y0, s1 = x1 + y1;
+            const i32x2 d = {__float_as_int(0.25f * s0), __float_as_int(0.25f * s1)};
+            __builtin_amdgcn_raw_buffer_store_b64(d, L[1].rsrc, (int)(q * 32u + 8u * g + soff(L[1], rp, 0)), 0, AUX_NT);
+            const float t = s0 + s1;
+            t2[rp >> 1] = (rp & 1) ? t2[rp >> 1] + t : t;
+        }
+        // level 2: lane g holds level-2 col g of rows 0 and 1
+#pragma unroll
+        for (int y2 = 0; y2 < 2; ++y2)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(0.0625f * t2[y2]), L[2].rsrc,
+                                                  (int)(q * 16u + 4u * g + soff(L[2], y2, 0)), 0, AUX_NT);
+        // level 3: col x3 = level-2 cols 2 x3, 2 x3 + 1 (lanes g, g ^ 1 = lane ^ 16); even g store
+        float t3 = t2[0] + t2[1];
+        t3 += __shfl_xor(t3, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int((1.0f / 64.0f) * t3), L[3].rsrc,
+                                              (int)((g & 1) ? kBig : q * 8u + 4u * (g >> 1) + soff(L[3], 0, 0)), 0, AUX_NT);
+    }
+}
+
+template <int ABL = 0>
+__global__ void __launch_bounds__(512, 1)
+corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
+                 const __bf16* __restrict__ bLo, PyrGeom g, int units, float* __restrict__ pyr) {
+    constexpr int WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = g.height, W = g.width, N = H * W;
     const int ncb = (W + kBlockCols - 1) / kBlockCols;
     const int nblk = ((H + kBlockRows - 1) / kBlockRows) * ncb;
     const int nqt = (N + 31) >> 5;
     const int u = xcd_block(blockIdx.x, gridDim.x);
-    if (u >= units) return;
+    if (u >= units) return;                                        // uniform per workgroup
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & 31, h = lane >> 5;
+    const int n = lane & 15, gq = lane >> 4;
     const int b = u / nblk, tb = u - b * nblk;
     const int rb = tb / ncb, cb = tb - rb * ncb;
     const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
 
-    // ---- A block (hi and lo) -> LDS: 32 pieces per thread, in two halves of 16 loads in flight ----
+    // ---- A block (hi and lo) -> LDS (k-major image), zero rows for targets outside the image -------
+    // piece id = tid + 512 i: lanes of an 8-lane group take 8 consecutive LDS rows of one chunk
+    // (conflict-free ds_write_b128), 8 such groups the 8 consecutive chunks of those pixels (128-B
+    // global segments)
     const size_t abase = (size_t)b * N * 256;
+    constexpr int kPieces = 2 * 32 * 128 / 512;                    // 16 per thread
+    uint4 v[kPieces];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        uint4 v[16];
+    for (int i = 0; i < kPieces; ++i) {
+        const int id = tid + i * 512;
+        const int r = (id & 7) + ((id >> 6) & 15) * 8;             // LDS row 0..127
+        const int cc = ((id >> 3) & 7) + ((id >> 10) & 3) * 8;     // channel chunk 0..31
+        const int part = id >> 12;
+        const int mt = r >> 4, ii = r & 15;
+        const int ty = ty0 + 2 * (mt >> 1) + (ii >> 3), tx = tx0 + 8 * (mt & 1) + (ii & 7);
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (ty < H && tx < W)
+            v[i] = *reinterpret_cast<const uint4*>((part ? aLo : aHi) + abase + (size_t)(ty * W + tx) * 256 + cc * 8);
+    }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int id = tid + (half * 16 + i) * 64 * WAVES;
-            const int row = id >> 6, c = id & 63;
-            const int ty = ty0 + (row >> 4), tx = tx0 + (row & 15);
-            const __bf16* src = c < 32 ? aHi : aLo;
-            v[i] = make_uint4(0, 0, 0, 0);
-            if (ty < H && tx < W) v[i] = *reinterpret_cast<const uint4*>(src + abase + (size_t)(ty * W + tx) * 256 + (c & 31) * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int id = tid + (half * 16 + i) * 64 * WAVES;
-            const int row = id >> 6, c = id & 63;
-            *reinterpret_cast<uint4*>(smem + (size_t)lds_row(row >> 4, row & 15) * kRow + (c < 32 ? 0 : 512) + (c & 31) * 16) = v[i];
-        }
+    for (int i = 0; i < kPieces; ++i) {
+        const int id = tid + i * 512;
+        const int r = (id & 7) + ((id >> 6) & 15) * 8;
+        const int cc = ((id >> 3) & 7) + ((id >> 10) & 3) * 8;
+        const int part = id >> 12;
+        *reinterpret_cast<uint4*>(smem + (size_t)((part * 32 + cc) * 128 + r) * 16) = v[i];
     }
     __syncthreads();
 
@@ -551,43 +677,47 @@ corr_pyramid_x3v2(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo
         L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
     }
 
-    unsigned b0 = (unsigned)j * kRow + 16u * h, b1 = b0 + 64u * kRow;
-    asm volatile("" : "+v"(b0), "+v"(b1));
-    const __bf16* bbase = bHi + ((size_t)b * nqt * 1024 + lane) * 8;
+    unsigned bhi = (unsigned)(gq * 128 + n) * 16u, blo = bhi + 65536u;
+    asm volatile("" : "+v"(bhi), "+v"(blo));
+    // B of 32-query tile qt: 16-query tiles 2 qt, 2 qt + 1 at bq + qt * 8192 (+ 4096 for the second)
+    const __bf16* bq = bHi + ((size_t)b * 2 * nqt * 512 + lane) * 8;
     const size_t lo_off = (size_t)(bLo - bHi);
-    constexpr int STEP = WAVES * QT;
-    // passes of this wave: tiles t0 + {0..QT-1} with t0 = w QT + STEP i; a tile past the map recomputes
-    // tile nqt - 1 (identical values rewritten)
-    const int npass = (nqt - w * QT + STEP - 1) / STEP;
-    bf16x8 rh[DR][QT], rl[DR][QT];
-    if (npass > 0) {
+    int qt = w;
+    bf16x8 rh[kDR16][2], rl[kDR16][2];
+    if (qt < nqt) {
+        const __bf16* p = bq + (size_t)qt * 8192;
 #pragma unroll
-        for (int qi = 0; qi < QT; ++qi) {
-            const __bf16* p = bbase + (size_t)min(w * QT + qi, nqt - 1) * 8192;
+        for (int s = 0; s < kDR16 - 1; ++s)
 #pragma unroll
-            for (int s = 0; s < DR - 1; ++s) {
-                rh[s][qi] = *reinterpret_cast<const bf16x8*>(p + 512 * s);
-                rl[s][qi] = *reinterpret_cast<const bf16x8*>(p + 512 * s + lo_off);
+            for (int uu = 0; uu < 2; ++uu) {
+                rh[s][uu] = *reinterpret_cast<const bf16x8*>(p + uu * 4096 + 512 * s);
+                rl[s][uu] = *reinterpret_cast<const bf16x8*>(p + uu * 4096 + 512 * s + lo_off);
             }
-        }
     }
-    vmcnt_pad_n<kEpiStores * QT>(pyr);
-    for (int i = 0; i < npass; ++i) {
-        const int t0 = w * QT + STEP * i;
-        const __bf16* cur[QT];
-        const __bf16* nxt[QT];
-#pragma unroll
-        for (int qi = 0; qi < QT; ++qi) {
-            cur[qi] = bbase + (size_t)min(t0 + qi, nqt - 1) * 8192;
-            nxt[qi] = bbase + (size_t)min(t0 + STEP + qi, nqt - 1) * 8192;
+    vmcnt_pad_n<kEpiStores16>(pyr);
+    // ping-pong phases as corr_pyramid_x3: waves w and w + 4 of each SIMD alternate MFMA and epilogue
+    const int nmax = (nqt + WAVES - 1) / WAVES;
+    const int nw = qt < nqt ? (nqt - qt + WAVES - 1) / WAVES : 0;
+    const bool late = w >= 4;
+    if (late) __builtin_amdgcn_s_barrier();
+    for (int k = 0; k < nmax; ++k) {
+        const int qn = qt + WAVES;
+        if (k < nw) {
+            f32x4 acc[8][2];
+            bf16x8 a0[8], a1[8];
+            read_a16<0, 0>(a0, smem, bhi, blo);
+            ksteps16<0>(acc, a0, a1, rh, rl, smem, bhi, blo, bq + (size_t)qt * 8192, bq + (size_t)min(qn, nqt - 1) * 8192,
+                        lo_off);
+            __builtin_amdgcn_s_barrier();
+            epilogue16(acc, L, qt, N, n, gq);
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_s_barrier();
         }
-        f32x16 acc[QT][4];
-        bf16x8 a0[8], a1[8];
-        read_a<0>(a0, smem, b0, b1);
-        v2_ksteps<QT, DR, 0>(acc, a0, a1, rh, rl, smem, b0, b1, cur, nxt, lo_off);
-#pragma unroll
-        for (int qi = 0; qi < QT; ++qi) epilogue(acc[qi], L, min((t0 + qi) * 32 + j, N - 1), h);
+        qt = qn;
     }
+    if (!late) __builtin_amdgcn_s_barrier();
 }
 
 }  // namespace
@@ -614,8 +744,9 @@ int prepare(const float* f1, const float* f2, int C, float scale, const rmd_pyra
     __bf16* bHi = aLo + (size_t)d.batch * N * 256;
     __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
     const int lds = 2 * kPx * kStride;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prep_split), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    prep_split<<<dim3((N + kPx - 1) / kPx, d.batch, 2), 512, lds, st>>>(f1, f2, aHi, aLo, bHi, bLo, C, N, nqt, scale);
+    auto kp = prep_split<RMD_X3_SHAPE == 16>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kp), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    kp<<<dim3((N + kPx - 1) / kPx, d.batch, 2), 512, lds, st>>>(f1, f2, aHi, aLo, bHi, bLo, C, N, nqt, scale);
     return check_launch("rmd_corr_prepare/x3");
 }
 
@@ -626,17 +757,16 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const __bf16* bHi = aLo + (size_t)d.batch * N * 256;
     const __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
     const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
-#if RMD_X3_V2
+#if RMD_X3_SHAPE == 16
     {
         const int units = nblk * d.batch;
-        const int lds = kBlockRows * kBlockCols * kRow;
-        auto kern = corr_pyramid_x3v2<RMD_X3_QT, RMD_X3_DR, RMD_X3_ABL>;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        kern<<<units, 256, lds, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<float*>(pyr));
-        return check_launch("rmd_corr_pyramid/gemm-x3v2");
+        auto kern = corr_pyramid_x3s<RMD_X3_ABL>;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds16);
+        kern<<<units, 512, kLds16, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<float*>(pyr));
+        return check_launch("rmd_corr_pyramid/gemm-x3");
     }
 #endif
-    // schedule (see corr_pyramid_x3): quarters Q in {1, 2, 4, 8} minimising slots x rounds per unit,
+    // schedule (32x32x16 form, -DRMD_X3_SHAPE=32) (see corr_pyramid_x3): quarters Q in {1, 2, 4, 8} minimising slots x rounds per unit,
     // slots = ceil(B nblk Q / CUs) (one 137-KB-LDS workgroup per CU), rounds = ceil(nqt / Q / 8); a
     // unit re-stages A, charged as 0.3 round.  Q = 1 with one workgroup per unit is the plain launch
     // (the only one when the grid is already several CU-loads deep).

@@ -21,6 +21,10 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     f1, f2, _ = bench.synthetic(8, 256, 55, 128, 1, 1234, "cuda")
+    fill = os.environ.get("X3_FILL", "")          # power check: 'zero' operands (DVFS give-back)
+    if fill == "zero":
+        f1.zero_()
+        f2.zero_()
     res = {"lib": os.path.basename(os.environ.get("RMD_LIBRARY", "librmd.so")), "precision": prec}
     ts = []
     pyr = None
