@@ -172,9 +172,11 @@ int rmd_corr_otf_lookup(const void* workspace, int batch, int channels, int heig
  * outputs are overwritten (B, C, H, W) float32.  C <= 256.  compute as in rmd_corr_otf_prepare
  * (RMD_F32 and RMD_BF16X3: split-bf16 products, fp32 accumulation; RMD_BF16: bf16 products).
  * Masked and 1-pixel levels and non-finite coordinates record no contribution.  `records` is a host
- * array of `nrecords` device pointers.  Deterministic in practice: records are summed in a fixed order,
- * and the pooled gradient adds per-workgroup fp32 tile sums in fp64 (exact, so order-independent,
- * while a target's contributions span < 2^29 in magnitude).
+ * array of `nrecords` device pointers.  Deterministic: records are summed in a fixed order, and the
+ * pooled gradient adds per-workgroup fp32 tile sums as 64-bit fixed point (integer atomics, associative,
+ * so bitwise order-independent for any dynamic range) at a power-of-two scale chosen per call from the
+ * largest recorded |weight| and |scale * fmap1| so that no sum can overflow; non-finite contributions
+ * propagate through a float side buffer.  A record carries a 256-B header after its weights.
  */
 size_t rmd_corr_otf_record_bytes(int batch, int height, int width, int levels, int radius);
 int rmd_corr_otf_record(const float* grad_out, const float* coords, int batch, int height, int width, int levels,
@@ -223,8 +225,9 @@ int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int heigh
 int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, int height, int width, int levels,
                             float scale, float* grad_fmap2, void* stream);
 
-/* The two GEMMs of the backward (autograd of the matmul at raft.py:31-33), fp32-accurate from three
- * split-bf16 MFMA products (hi.hi + hi.lo + lo.hi), batched over `batch`:
+/* The two GEMMs of the backward (autograd of the matmul at raft.py:31-33), batched over `batch`;
+ * compute RMD_BF16X3: fp32-accurate from three split-bf16 MFMA products (hi.hi + hi.lo + lo.hi, the fp32
+ * precision modes); RMD_BF16: one bf16 product per k-step, fp32 accumulation (the bf16 mode):
  *   out[b] (m x nc, row-major) = a[b] (m x k, row stride lda) . B[b]
  *   layout 0: B element (k, n) at bm[k*ldb + n]                 (k x nc, ldb >= nc)
  *   layout 1: B element (k, n) at bm[n*ldb + k]                 (nc x k, ldb >= k)
@@ -236,7 +239,7 @@ int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, i
  * (0 = none needed) and a second pass sums the partial tiles in a fixed order (deterministic). */
 size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, int nc);
 int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m, int k, int nc,
-                       int layout, float* out, void* workspace, void* stream);
+                       int layout, int compute, float* out, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);

@@ -82,7 +82,9 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ at, int k, int
 // from the current buffer; the barrier at the bottom publishes chunk c+1 and frees buffer c for c+2.
 // A global load thus has a whole chunk of MFMAs (two, for its first use) to land, and the hi / lo split
 // of the next chunk runs beside the current chunk's MFMAs (waves 0-3 and 4-7 share each SIMD).
-template <bool VA, bool VB, int LAYOUT>
+// X3 = false (compute RMD_BF16, the bf16 precision mode): one bf16 product per k-step (hi.hi), the lo
+// halves are neither split nor stored
+template <bool VA, bool VB, int LAYOUT, bool X3 = true>
 __global__ void __launch_bounds__(512, 1)
 grad_gemm_x3(GemmArgs p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -152,7 +154,7 @@ grad_gemm_x3(GemmArgs p) {
             split4(ra[it].x, ra[it].y, ra[it].z, ra[it].w, hi, lo);
             unsigned char* d = sA + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
             *reinterpret_cast<bf16x4*>(d) = hi;
-            *reinterpret_cast<bf16x4*>(d + 64) = lo;
+            if constexpr (X3) *reinterpret_cast<bf16x4*>(d + 64) = lo;
         }
         if constexpr (LAYOUT == 0 || LAYOUT == 2) {
             // transpose: column 4nq + j of the thread's 2 k rows -> LDS row of that column, k offset 2kq
@@ -167,7 +169,7 @@ grad_gemm_x3(GemmArgs p) {
                 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
                 unsigned char* d = sB + (nr + j) * kRowB + kq * 4;
                 *reinterpret_cast<bf16x2*>(d) = bf16x2{h0, h1};
-                *reinterpret_cast<bf16x2*>(d + 64) = bf16x2{l0, l1};
+                if constexpr (X3) *reinterpret_cast<bf16x2*>(d + 64) = bf16x2{l0, l1};
             }
         } else {
 #pragma unroll
@@ -176,7 +178,7 @@ grad_gemm_x3(GemmArgs p) {
                 split4(rb[it].x, rb[it].y, rb[it].z, rb[it].w, hi, lo);
                 unsigned char* d = sB + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
                 *reinterpret_cast<bf16x4*>(d) = hi;
-                *reinterpret_cast<bf16x4*>(d + 64) = lo;
+                if constexpr (X3) *reinterpret_cast<bf16x4*>(d + 64) = lo;
             }
         }
     };
@@ -211,17 +213,21 @@ grad_gemm_x3(GemmArgs p) {
                 const unsigned char* pa = cur + aoff + i * 32 * kRowB + s * 32;
                 const unsigned char* pb = cur + boff + i * 32 * kRowB + s * 32;
                 ah[i] = *reinterpret_cast<const bf16x8*>(pa);
-                al[i] = *reinterpret_cast<const bf16x8*>(pa + 64);
                 bh[i] = *reinterpret_cast<const bf16x8*>(pb);
-                bl[i] = *reinterpret_cast<const bf16x8*>(pb + 64);
+                if constexpr (X3) {
+                    al[i] = *reinterpret_cast<const bf16x8*>(pa + 64);
+                    bl[i] = *reinterpret_cast<const bf16x8*>(pb + 64);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     f32x16 t = acc[i][j];
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t, 0, 0, 0);
+                    if constexpr (X3) {
+                        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], t, 0, 0, 0);
+                    }
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], t, 0, 0, 0);
                 }
         }
@@ -299,8 +305,8 @@ Plan plan(int batch, int M, int K, int Nc) {
 }
 
 template <bool VA, bool VB, int LAYOUT>
-void launch_gemm(const GemmArgs& a, int nwg, hipStream_t st) {
-    auto k = grad_gemm_x3<VA, VB, LAYOUT>;
+void launch_gemm(const GemmArgs& a, int nwg, bool x3, hipStream_t st) {
+    auto k = x3 ? grad_gemm_x3<VA, VB, LAYOUT, true> : grad_gemm_x3<VA, VB, LAYOUT, false>;
     // the >64 KB LDS opt-in is per device: set it before every launch (cheap host call), so a process
     // that launches on a second GPU gets it too
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -318,8 +324,11 @@ extern "C" size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, in
 }
 
 extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m,
-                                  int k, int nc, int layout, float* out, void* workspace, void* stream) {
+                                  int k, int nc, int layout, int compute, float* out, void* workspace, void* stream) {
     RMD_REQUIRE(a && bm && out, RMD_ERR_ARG, "rmd_corr_grad_gemm: null pointer");
+    RMD_REQUIRE(compute == RMD_BF16X3 || compute == RMD_BF16, RMD_ERR_ARG,
+                "rmd_corr_grad_gemm: compute must be RMD_BF16X3 or RMD_BF16");
+    const bool x3 = compute == RMD_BF16X3;
     RMD_REQUIRE(batch > 0 && m > 0 && k > 0 && nc > 0, RMD_ERR_SHAPE, "rmd_corr_grad_gemm: empty shape");
     RMD_REQUIRE(layout >= 0 && layout <= 3, RMD_ERR_ARG, "rmd_corr_grad_gemm: layout must be 0..3");
     RMD_REQUIRE(lda >= k && ldb >= (layout == 0 ? nc : layout == 3 ? nc : k), RMD_ERR_SHAPE,
@@ -358,10 +367,10 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     const bool va = a16 && (lda & 3) == 0;
     bool vb = b16 && (ldb & 3) == 0;
 #define RMD_GG(VA, VB)                                                                      \
-    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, st)                             \
-     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, st)                           \
-     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, st)                           \
-                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, st))
+    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, x3, st)                         \
+     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, x3, st)                       \
+     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, x3, st)                       \
+                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, x3, st))
     if (layout >= 2) vb = b16;                 // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
     if (va && vb) RMD_GG(true, true);
     else if (va) RMD_GG(true, false);

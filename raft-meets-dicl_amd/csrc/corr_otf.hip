@@ -100,7 +100,8 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_ILV
 #define RMD_OTF_ILV 1
 #endif
-// backward ablation for A/B timing only (wrong results): 1 = the dP atomic adds are skipped
+// backward ablation for A/B timing only (wrong results): 1 = the dP atomic adds are skipped, 2 = the G
+// build reads no record weights (constants instead)
 #ifndef RMD_OTF_BWD_ABL
 #define RMD_OTF_BWD_ABL 0
 #endif
@@ -596,26 +597,35 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
 // Every lookup of a block records its patch weights (otf_record_kernel: origin + K*K weights per
 // (level, query), no volume); one launch after the last lookup backward turns all records into the
 // two products, so the box of target rows a query tile touches is swept once for all iterations:
-//  * one 512-thread workgroup per 32 x 4 query tile; per level the union box of the tile's patches
-//    over all records, swept in bands of one target row x kBwdTB columns;
-//  * only the target rows some record patch covers are swept, each over its covered column extent;
-//  * per band the dense G (128 queries x kBwdTB targets, fp32) is built in LDS, one thread per (query,
-//    column) summing the records in order (deterministic);
+//  * one 512-thread workgroup per 32 x 4 query tile; per level the target rows some record patch covers,
+//    each over its covered column extent (per-row extents: a divergent flow costs its patches' rows);
+//  * those rows' 16-column target segments are packed in order into bands of up to 8 segments (128
+//    targets, possibly spanning several rows): fewer, longer MFMA phases than one band per row;
+//  * per band the dense G (128 queries x 128 band targets, fp32) is built in LDS by owner threads:
+//    thread (query q, p) owns the band columns = p (mod 4) of its query's row and adds, record by
+//    record in order, the patch weights that land there (deterministic; a wave's loads run along the
+//    queries of its own patch column: coalesced);
 //  * d q~ (128 queries x C) += G . P_band: v_mfma_f32_32x32x16_bf16 with A = G rows from LDS and B =
-//    the band's targets in the "T layout" (lane c + 32h holds pixels 8h..8h+7 of channel c of a 16-pixel
-//    segment: the B fragment of a 16-target k-step), accumulated in registers over all bands;
-//  * d P_band (kBwdTB targets x C) = G^T . q~: A = G columns from LDS, B = the tile's queries in the T
-//    layout; the 32 x 32 result tiles (fp32) are added to a pixel-major fp64 d P with float64 atomics:
-//    the fp64 sum of fp32 tile sums is exact — so independent of the order the workgroups add in — as
-//    long as a target's contributions span less than 2^29 in magnitude, and below that the fp64
-//    rounding (2^-53) stays far under the fp32 result's ulp (run-to-run equal in the tests).
+//    the band's target segments in the "T layout" (lane c + 32h holds pixels 8h..8h+7 of channel c of a
+//    16-pixel segment), the next segment's fragments loaded while the current one's MFMAs run;
+//  * d P_band = G^T . q~: A = G columns from LDS, B = the tile's query segments (bf16: copied to LDS
+//    once per workgroup; split-bf16: from L2, one k-step ahead); every fp32 32 x 32 result tile is added
+//    to d P as 64-bit fixed point with integer atomics.  Integer addition is associative, so d P is
+//    bitwise independent of the order the workgroups add in — with no premise on the contributions'
+//    dynamic range.  The scale 2^s is a power of two chosen per backward from the largest |weight|
+//    (recorded by otf_record_kernel) and |q~| (otf_tlayout_kernel) so that no sum can exceed 2^62:
+//    |d P| <= records * N * max|w| * max|q~|; the fixed-point step 2^-s is ~2^-40 of that bound,
+//    far below the fp32 ulp of any element the bound lets reach 2^-15 of it.  Non-finite contributions
+//    go to a float side buffer instead (NaN / inf propagate as through the reference's autograd).
 // fp32 modes split G and both operands into bf16 hi + lo and accumulate lo.hi + hi.lo + hi.hi (the
 // forward x3 split); bf16 mode uses one product.
 constexpr int kBwdQX = 32, kBwdQY = 4, kBwdQ = kBwdQX * kBwdQY;
-constexpr int kBwdTB = 128;                          // band width (targets)
+constexpr int kBwdSeg = 8;                           // 16-target segments per band
+constexpr int kBwdTB = 16 * kBwdSeg;                 // band width (targets)
+constexpr int kBwdRows = 4;                          // distinct target rows per band (G-build registers)
 constexpr int kBwdLd = kBwdTB + 4;                   // G row stride (floats): conflict-free row and column reads
 constexpr int kBwdThreads = 512;
-constexpr int kMaxRec = 32;                          // records per launch (more: several launches)
+constexpr int kMaxRec = 16;                          // records per launch (more: several launches)
 constexpr int kFar = -(1 << 29);                     // origin of a masked / degenerate level
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -629,29 +639,45 @@ struct OtfRecords {
 size_t otf_record_org_bytes(int B, int H, int W, int L) {
     return ((size_t)L * B * H * W * sizeof(int2) + 255) / 256 * 256;
 }
+size_t otf_record_wp_bytes(int B, int H, int W, int L, int K) {
+    return ((size_t)L * B * H * W * K * K * sizeof(float) + 255) / 256 * 256;
+}
+
+// |v| as ordered integer bits for an atomicMax of finite magnitudes (non-finite values are skipped);
+// dst is an array of kMaxSlots words, each workgroup adds into slot blockIdx % kMaxSlots (one
+// address per thousands of waves would serialise the atomics)
+constexpr int kMaxSlots = 64;
+__device__ __forceinline__ void max_abs_finite(unsigned* dst, float v) {
+    unsigned m = __builtin_isfinite(v) ? (__float_as_uint(v) & 0x7fffffffu) : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(dst + blockIdx.x % kMaxSlots, m);
+}
 
 // per (level, batch, query): origin and the (2r+2)^2 patch weights of grad_out's window
 //   wp[j][k] = (1-fy) hx(k, j) + fy hx(k, j-1),  hx(k, bb) = (1-fx) g[k][bb] + fx g[k-1][bb]
 // (g[a][bb] = grad_out channel l*D*D + a*D + bb; out-of-range a / bb -> 0).  Masked and 1-pixel levels
 // record kFar (no contribution); a non-finite coordinate clamps far off the map (no contribution).
+// The largest finite |weight| goes to *wmax (the record's header word, zeroed by the launcher).
 template <int R>
 __global__ void __launch_bounds__(kThreads)
 otf_record_kernel(const float* __restrict__ gout, const float* __restrict__ coords, OtfGeom g, unsigned zmask,
-                  int2* __restrict__ org, float* __restrict__ wp) {
+                  int2* __restrict__ org, float* __restrict__ wp, unsigned* __restrict__ wmax) {
     constexpr int D = 2 * R + 1, K = 2 * R + 2;
     const long long N = (long long)g.H * g.W;
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    if (idx >= (long long)g.L * g.B * N) return;
-    const int q = (int)(idx % N);
-    const int b = (int)((idx / N) % g.B);
-    const int l = (int)(idx / (N * g.B));
+    const bool in = idx < (long long)g.L * g.B * N;
+    const long long id = in ? idx : 0;
+    const int q = (int)(id % N);
+    const int b = (int)((id / N) % g.B);
+    const int l = (int)(id / (N * g.B));
     const int lh = g.lh[l], lw = g.lw[l];
     const float x = coords[((size_t)b * 2 + 0) * N + q], y = coords[((size_t)b * 2 + 1) * N + q];
     const float inv = 1.0f / (float)(1 << l);
     const float rx = x * inv, ry = y * inv;
     const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f), cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
-    const bool dead = ((zmask >> l) & 1u) || lh < 2 || lw < 2 || !(rx == rx) || !(ry == ry);
-    org[idx] = dead ? make_int2(kFar, kFar) : make_int2((int)floorf(cx) - R, (int)floorf(cy) - R);
+    const bool dead = !in || ((zmask >> l) & 1u) || lh < 2 || lw < 2 || !(rx == rx) || !(ry == ry);
+    if (in) org[id] = dead ? make_int2(kFar, kFar) : make_int2((int)floorf(cx) - R, (int)floorf(cy) - R);
     const float fx = rx - floorf(rx), fy = ry - floorf(ry);
     const float* gp = gout + ((size_t)b * g.L + l) * D * D * N + q;
     float gv[D][D];
@@ -660,6 +686,7 @@ otf_record_kernel(const float* __restrict__ gout, const float* __restrict__ coor
 #pragma unroll
         for (int bb = 0; bb < D; ++bb) gv[a][bb] = dead ? 0.f : gp[(size_t)(a * D + bb) * N];
     float* w = wp + ((size_t)l * g.B + b) * K * K * N + q;
+    float m = 0.f;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
 #pragma unroll
@@ -669,24 +696,28 @@ otf_record_kernel(const float* __restrict__ gout, const float* __restrict__ coor
                 const float v0 = k < D ? gv[k][bb] : 0.f, v1 = k >= 1 ? gv[k - 1][bb] : 0.f;
                 return (1.f - fx) * v0 + fx * v1;
             };
-            const float v = (1.f - fy) * hx(j) + fy * hx(j - 1);
-            w[(size_t)(j * K + k) * N] = dead ? 0.f : v;
+            const float v = dead ? 0.f : (1.f - fy) * hx(j) + fy * hx(j - 1);
+            if (in) w[(size_t)(j * K + k) * N] = v;
+            m = __builtin_isfinite(v) ? fmaxf(m, fabsf(v)) : m;
         }
     }
+    max_abs_finite(wmax, m);
 }
 
 // T layout of a planar (B, C, h, w) fp32 map (times s): unit (b, level segment row/seg, channel group cg)
 // = 64 lanes x 8 elements, lane c + 32h = pixels 8h..8h+7 of channel 32cg + c (zero past the map / C);
-// X3: the unit's lo half follows its hi half.  One thread per (unit, lane).
+// X3: the unit's lo half follows its hi half.  One thread per (unit, lane).  vmax (optional): the
+// largest finite |value| (the query operand's, for the fixed-point scale of d P).
 template <bool X3>
 __global__ void __launch_bounds__(kThreads)
-otf_tlayout_kernel(LevelSrc src, OtfGeom g, float s, __bf16* __restrict__ dst) {
+otf_tlayout_kernel(LevelSrc src, OtfGeom g, float s, __bf16* __restrict__ dst, unsigned* __restrict__ vmax) {
     constexpr int NP = X3 ? 2 : 1;
     const int ncg = g.Cp / 32;
     const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    if (idx >= (long long)g.B * g.TS * ncg * 64) return;
-    const int lane = (int)(idx & 63), c32 = lane & 31, h = lane >> 5;
-    const long long u = idx >> 6;
+    const bool in = idx < (long long)g.B * g.TS * ncg * 64;
+    const long long id = in ? idx : 0;
+    const int lane = (int)(id & 63), c32 = lane & 31, h = lane >> 5;
+    const long long u = id >> 6;
     const int cg = (int)(u % ncg);
     const long long bs = u / ncg;
     const long long sg = bs % g.TS;
@@ -701,15 +732,30 @@ otf_tlayout_kernel(LevelSrc src, OtfGeom g, float s, __bf16* __restrict__ dst) {
     const size_t plane = (size_t)g.lh[l] * g.lw[l];
     const float* row = src.p[l] + ((size_t)b * g.C + (c < g.C ? c : 0)) * plane + (size_t)y * g.lw[l];
     bf16x8 hi, lo;
+    float m = 0.f;
+    float xv[8];
+    const bool cin = in && c < g.C;
+    if (cin && x0 + 8 <= g.lw[l] && ((((uintptr_t)(row + x0)) & 15) == 0)) {
+        // whole 8-pixel run: two 16-B loads (the per-element path below is the map's right edge)
+        *reinterpret_cast<float4*>(xv) = *reinterpret_cast<const float4*>(row + x0);
+        *reinterpret_cast<float4*>(xv + 4) = *reinterpret_cast<const float4*>(row + x0 + 4);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = (cin && x0 + e < g.lw[l]) ? row[x0 + e] : 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        const float v = (c < g.C && x0 + e < g.lw[l]) ? row[x0 + e] * s : 0.f;
+        const float v = cin ? xv[e] * s : 0.f;
         hi[e] = (__bf16)v;
         lo[e] = (__bf16)(v - (float)hi[e]);
+        m = __builtin_isfinite(v) ? fmaxf(m, fabsf(v)) : m;
     }
-    __bf16* o = dst + ((size_t)u * NP * 64 + lane) * 8;
-    *reinterpret_cast<bf16x8*>(o) = hi;
-    if constexpr (X3) *reinterpret_cast<bf16x8*>(o + 64 * 8) = lo;
+    if (in) {
+        __bf16* o = dst + ((size_t)u * NP * 64 + lane) * 8;
+        *reinterpret_cast<bf16x8*>(o) = hi;
+        if constexpr (X3) *reinterpret_cast<bf16x8*>(o + 64 * 8) = lo;
+    }
+    if (vmax) max_abs_finite(vmax, m);
 }
 
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
@@ -735,39 +781,88 @@ struct BwdArgs {
     const __bf16* pt;           // targets, T layout (B, TS, ncg units)
     const __bf16* qt;           // queries (fmap1 * scale), T layout (B, QS, ncg units)
     OtfRecords rec;
-    double* dP;                 // (B, PT, C) pixel-major fp64, += G^T q~ (fp32 tile sums added in fp64)
+    long long* dP;              // (B, PT, C) pixel-major fixed point (2^-s units), += G^T q~
+    float* dPnf;                // (B, PT, C) non-finite contributions (float atomics; zero otherwise)
     long long pT;               // pooled pixels per batch (all levels)
     long long poff[RMD_MAX_LEVELS];
     float* gq;                  // (B, C, H, W) fp32, += scale * G P
     float scale;
+    const int* sexp;            // fixed-point exponent s of d P (otf_fixed_exp_kernel)
+    int* nf;                    // set when any contribution went to dPnf
 };
+
+struct BwdWmax {                // header words of up to kMaxRecAll records (the scale's bound)
+    const unsigned* p[64];
+};
+
+// fixed-point exponent s: 2^s * bound <= 2^62 with bound = nrec * N * max|w| * max|q~| (a power of two
+// scale, the same for every workgroup: deterministic)
+__device__ __forceinline__ int fixed_exp(float bound) {
+    if (!(bound > 0.f) || !__builtin_isfinite(bound)) return 60;
+    int e;
+    (void)frexpf(bound, &e);                         // bound < 2^e
+    return max(-960, min(960, 62 - e));
+}
 
 template <bool X3, int R>
 __global__ void __launch_bounds__(kBwdThreads, 1)
 otf_backward_kernel(BwdArgs a) {
     constexpr int K = 2 * R + 2;
     constexpr int NP = X3 ? 2 : 1;
-    extern __shared__ float G[];                                     // [kBwdQ][kBwdLd], then rowext
-    int2* rowext = reinterpret_cast<int2*>(G + kBwdQ * kBwdLd);      // [level-0 rows]
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    float* G = reinterpret_cast<float*>(dyn);                              // [kBwdQ][kBwdLd]
+    __bf16* qimg = reinterpret_cast<__bf16*>(dyn + sizeof(float) * kBwdQ * kBwdLd);   // bf16: [8][ncg][64][8]
     __shared__ int2 sorg[kMaxRec][kBwdQ];
     __shared__ int box[4];
+    __shared__ int bseg_row[kBwdSeg], bseg_x[kBwdSeg];
+    __shared__ int bnseg, bcur_row, bcur_x, bnrow;
+    __shared__ int brow_y[kBwdRows], brow_s0[kBwdRows], brow_x0[kBwdRows], brow_n[kBwdRows];
+    __shared__ const int2* s_org[kMaxRec];
+    __shared__ const float* s_wp[kMaxRec];
     const OtfGeom& g = a.g;
     const int N = g.H * g.W;
+    const int ncg = g.Cp / 32;
     const int nbx = (g.W + kBwdQX - 1) / kBwdQX, nqb = nbx * ((g.H + kBwdQY - 1) / kBwdQY);
     const int lid = xcd_block(blockIdx.x, gridDim.x);
     const int qb = lid % nqb, b = lid / nqb;
     const int qx0 = (qb % nbx) * kBwdQX, qy0 = (qb / nbx) * kBwdQY;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int j32 = lane & 31, h = lane >> 5;
-    const int ncg = g.Cp / 32;
     const int mt = w & 3;                                            // query row / target tile of this wave
     const int nt0 = (w >> 2) * 4;                                    // first channel tile of this wave
     const int ntn = max(0, min(4, ncg - nt0));
     const size_t unit = (size_t)64 * 8 * NP;                         // elements per T-layout unit
+    int2* rowext = reinterpret_cast<int2*>(dyn + sizeof(float) * kBwdQ * kBwdLd + (X3 ? 0 : (size_t)8 * ncg * 1024));
+    // G build ownership: thread (query gq_, class p) owns band columns = p (mod 4); the 4 classes of a
+    // query are adjacent lanes, so a wave's weight load reads 16 consecutive queries of 4 patch columns
+    const int gq_ = tid >> 2, p = tid & 3;
+    const int gy = qy0 + gq_ / kBwdQX, gx = qx0 + gq_ % kBwdQX;
+    const bool gvalid = gy < g.H && gx < g.W;
+    const size_t qoff = gvalid ? (size_t)gy * g.W + gx : 0;
 
+    // bf16: the tile's query segments (8 x ncg units) -> LDS once (the B operand of every d P phase)
+    if constexpr (!X3) {
+        for (int i = tid; i < 8 * ncg * 64; i += kBwdThreads) {
+            const int un = i >> 6, ln = i & 63;
+            const int qs = un / ncg, cg = un % ncg;
+            const int qrow = qy0 + (qs >> 1), qsx = (qx0 >> 4) + (qs & 1);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (qrow < g.H && qsx < g.qnsx)
+                v = *reinterpret_cast<const uint4*>(a.qt + ((size_t)(b * g.QS + qrow * g.qnsx + qsx) * ncg + cg) * unit + ln * 8);
+            *reinterpret_cast<uint4*>(qimg + (size_t)i * 8) = v;
+        }
+    }
+
+    // record pointers to LDS (runtime-indexed kernel-argument arrays would sit in SGPRs and spill)
+    if (tid < kMaxRec) {
+        s_org[tid] = tid < a.rec.n ? a.rec.org[tid] : nullptr;
+        s_wp[tid] = tid < a.rec.n ? a.rec.wp[tid] : nullptr;
+    }
+    const int nrec = a.rec.n;
     f32x16 accq[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) accq[t] = f32x16{};
+    const double fscale = ldexp(1.0, *a.sexp);
 
     for (int l = 0; l < g.L; ++l) {
         const int lh = g.lh[l], lw = g.lw[l];
@@ -775,11 +870,11 @@ otf_backward_kernel(BwdArgs a) {
         __syncthreads();                                             // previous level's G / sorg reads done
         if (tid < 4) box[tid] = (tid & 1) ? -(1 << 30) : (1 << 30);
         __syncthreads();
-        for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
+        for (int i = tid; i < nrec * kBwdQ; i += kBwdThreads) {
             const int r = i / kBwdQ, q = i % kBwdQ;
             const int y = qy0 + q / kBwdQX, x = qx0 + q % kBwdQX;
             int2 o = make_int2(kFar, kFar);
-            if (y < g.H && x < g.W) o = a.rec.org[r][((size_t)l * g.B + b) * N + y * g.W + x];
+            if (y < g.H && x < g.W) o = s_org[r][((size_t)l * g.B + b) * N + y * g.W + x];
             // patches entirely off the map contribute nothing
             if (o.x + K - 1 < 0 || o.x >= lw || o.y + K - 1 < 0 || o.y >= lh) o = make_int2(kFar, kFar);
             sorg[r][q] = o;
@@ -793,12 +888,14 @@ otf_backward_kernel(BwdArgs a) {
         __syncthreads();
         const int bx0 = box[0], bx1 = box[1], by0 = box[2], by1 = box[3];
         if (bx0 > bx1) continue;                                     // uniform: nothing at this level
-        // per target row of the box, the column extent of the record patches that cover it: bands of
-        // rows (and columns) no patch touches are skipped, so a divergent flow costs its patches' rows,
-        // not the whole union box
+        // per target row of the box, the column extent of the record patches that cover it
         for (int i = tid; i <= by1 - by0; i += kBwdThreads) rowext[i] = make_int2(1 << 30, -(1 << 30));
+        if (tid == 0) {
+            bcur_row = by0;
+            bcur_x = -1;
+        }
         __syncthreads();
-        for (int i = tid; i < a.rec.n * kBwdQ; i += kBwdThreads) {
+        for (int i = tid; i < nrec * kBwdQ; i += kBwdThreads) {
             const int2 o = sorg[i / kBwdQ][i % kBwdQ];
             if (o.x == kFar) continue;
             const int x0 = max(o.x, 0), x1 = min(o.x + K - 1, lw - 1);
@@ -807,90 +904,190 @@ otf_backward_kernel(BwdArgs a) {
                 atomicMax(&rowext[j - by0].y, x1);
             }
         }
-        __syncthreads();
         const __bf16* plev = a.pt + ((size_t)b * g.TS + g.soff[l]) * ncg * unit;
-        for (int ty = by0; ty <= by1; ++ty) {
-            const int2 ext = rowext[ty - by0];                       // uniform
-            if (ext.x > ext.y) continue;
-            for (int cx = ext.x & ~15; cx <= ext.y; cx += kBwdTB) {
-                const int ncols = min(kBwdTB, ((ext.y - cx + 1) + 15) & ~15);
-                // ---- G (queries x band targets) from every record's patch row ty -----------------------
-                // one thread per (query, column) sums the records in order: deterministic, no atomics;
-                // columns up to the next multiple of 32 are written (zero) for the 32-wide dP tiles
-                __syncthreads();                                     // previous band's G reads done
-                const int ncols32 = (ncols + 31) & ~31;
-                for (int i = tid; i < kBwdQ * ncols32; i += kBwdThreads) {
-                    const int col = i % ncols32, q = i / ncols32;
-                    const int tx = cx + col;
-                    float sum = 0.f;
-                    if (col < ncols && tx < lw) {
-                        const size_t qoff = (size_t)(qy0 + q / kBwdQX) * g.W + qx0 + q % kBwdQX;
-                        for (int r = 0; r < a.rec.n; ++r) {
-                            const int2 o = sorg[r][q];
-                            const int j = ty - o.y, k = tx - o.x;
-                            if (o.x != kFar && j >= 0 && j < K && k >= 0 && k < K)
-                                sum += a.rec.wp[r][(((size_t)l * g.B + b) * K * K + j * K + k) * N + qoff];
+        for (;;) {
+            // ---- next band: up to kBwdSeg segments (row, 16-column segment) in row-major order -------
+            __syncthreads();                                         // rowext ready / previous band's G reads done
+            if (tid == 0) {
+                // segments join in row-major order; a band holds at most kBwdSeg segments in at most
+                // kBwdRows rows (consecutive segment columns within a row)
+                int n = 0, nr = 0, ty = bcur_row, sx = bcur_x;   // sx < 0: start of row ty
+                while (n < kBwdSeg && ty <= by1) {
+                    const int2 e = rowext[ty - by0];
+                    if (e.x > e.y) { ++ty; sx = -1; continue; }
+                    if (sx < 0) sx = e.x >> 4;
+                    if (sx > (e.y >> 4)) { ++ty; sx = -1; continue; }
+                    if (nr == 0 || brow_y[nr - 1] != ty) {
+                        if (nr == kBwdRows) break;
+                        brow_y[nr] = ty;
+                        brow_s0[nr] = n;
+                        brow_x0[nr] = sx;
+                        brow_n[nr] = 0;
+                        ++nr;
+                    }
+                    bseg_row[n] = ty;
+                    bseg_x[n] = sx;
+                    ++brow_n[nr - 1];
+                    ++n;
+                    ++sx;
+                }
+                bnseg = n;
+                bnrow = nr;
+                bcur_row = ty;
+                bcur_x = sx;
+            }
+            __syncthreads();
+            const int nseg = bnseg, bnrow_ = bnrow;                  // uniform
+            if (nseg == 0) break;
+            // ---- G (queries x band targets): owner threads, records in order ----------------------
+            // zero this thread's columns (band columns = p mod 4 of row gq_), then add every record's
+            // patch weights that land in them
+            float* grow = G + gq_ * kBwdLd;
+            for (int c = p; c < kBwdTB; c += 4) grow[c] = 0.f;
+            if (gvalid) {
+                // records in batches of kRB: every weight load of a batch is issued before the first
+                // add (one memory latency per batch, not one per record and row), then the adds in record
+                // order (each G element receives at most one weight per record)
+                constexpr int kRB = 4, KM = (K + 3) / 4;
+                const size_t lofs = ((size_t)l * g.B + b) * K * K * N + qoff;
+                for (int r0 = 0; r0 < nrec; r0 += kRB) {
+                    float v[kRB][kBwdRows][KM];
+#pragma unroll
+                    for (int ri = 0; ri < kRB; ++ri) {
+                        const int r = r0 + ri;
+                        const int2 o = r < nrec ? sorg[r][gq_] : make_int2(kFar, kFar);
+                        const float* wq = s_wp[r < nrec ? r : 0] + lofs;
+                        const int k0 = (p - o.x) & 3;
+#pragma unroll
+                        for (int br = 0; br < kBwdRows; ++br) {
+                            const int jr = brow_y[br] - o.y;
+                            const bool rok = br < bnrow_ && o.x != kFar && jr >= 0 && jr < K;
+#pragma unroll
+                            for (int m = 0; m < KM; ++m) {
+                                const int k = k0 + 4 * m;
+                                const int tx = o.x + k;
+                                const int si = (tx >> 4) - brow_x0[br];
+                                const bool ok = rok && k < K && tx >= 0 && tx < lw && si >= 0 && si < brow_n[br];
+                                v[ri][br][m] = ok ? (RMD_OTF_BWD_ABL == 2 ? 1e-3f * (float)(k + jr)
+                                                                          : wq[(size_t)(jr * K + k) * N])
+                                                  : 0.f;
+                            }
                         }
                     }
-                    G[q * kBwdLd + col] = sum;
+#pragma unroll
+                    for (int ri = 0; ri < kRB; ++ri) {
+                        const int r = r0 + ri;
+                        const int2 o = r < nrec ? sorg[r][gq_] : make_int2(kFar, kFar);
+                        const int k0 = (p - o.x) & 3;
+#pragma unroll
+                        for (int br = 0; br < kBwdRows; ++br) {
+                            const int jr = brow_y[br] - o.y;
+                            const bool rok = br < bnrow_ && o.x != kFar && jr >= 0 && jr < K;
+#pragma unroll
+                            for (int m = 0; m < KM; ++m) {
+                                const int k = k0 + 4 * m;
+                                const int tx = o.x + k;
+                                const int si = (tx >> 4) - brow_x0[br];
+                                if (rok && k < K && tx >= 0 && tx < lw && si >= 0 && si < brow_n[br])
+                                    grow[16 * (brow_s0[br] + si) + (tx & 15)] += v[ri][br][m];
+                            }
+                        }
+                    }
                 }
-                __syncthreads();
-                // ---- d q~ += G . P_band (query tile mt, channel tiles nt0..nt0+ntn-1) ------------------
-                for (int ks = 0; ks < ncols / 16; ++ks) {
-                    const float* gr = G + (mt * 32 + j32) * kBwdLd + ks * 16 + 8 * h;
+            }
+            __syncthreads();
+            // ---- d q~ += G . P_band (query tile mt, channel tiles nt0..nt0+ntn-1) ------------------
+            // rolling fragment ring: channel tile t's fragments of segment s + 1 are loaded right after
+            // its MFMAs of segment s (one buffer of 4 (x2) fragments, each load covered by the other
+            // tiles' MFMAs)
+            if (ntn > 0) {
+                bf16x8 bh[4], bl[4];
+                const size_t seg_unit = (size_t)ncg * unit;
+                auto seg_ptr = [&](int s) {
+                    return plev + (size_t)(bseg_row[s] * g.nsx[l] + bseg_x[s]) * seg_unit + lane * 8;
+                };
+                const __bf16* pu = seg_ptr(0);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const __bf16* pp = pu + (size_t)(nt0 + min(t, ntn - 1)) * unit;
+                    bh[t] = *reinterpret_cast<const bf16x8*>(pp);
+                    bl[t] = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh[t];
+                }
+                for (int s = 0; s < nseg; ++s) {
+                    const float* gr = G + (mt * 32 + j32) * kBwdLd + s * 16 + 8 * h;
                     float v[8];
                     *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(gr);
                     *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(gr + 4);
                     bf16x8 ah, al;
                     split8(v, ah, al);
-                    const __bf16* pu = plev + ((size_t)(ty * g.nsx[l] + (cx >> 4) + ks) * ncg) * unit + lane * 8;
+                    const __bf16* pn = seg_ptr(min(s + 1, nseg - 1));
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        if (t >= ntn) break;
-                        const __bf16* pp = pu + (size_t)(nt0 + t) * unit;
-                        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pp);
-                        const bf16x8 bl = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh;
-                        mma3<X3>(accq[t], ah, al, bh, bl);
+                        if (t < ntn) mma3<X3>(accq[t], ah, al, bh[t], bl[t]);
+                        const __bf16* pp = pn + (size_t)(nt0 + min(t, ntn - 1)) * unit;
+                        bh[t] = *reinterpret_cast<const bf16x8*>(pp);
+                        bl[t] = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh[t];
                     }
                 }
-                // ---- d P_band = G^T . q~ (target tile mt, channel tiles nt0..), float atomics ------------
-                if (mt * 32 < ncols && ntn > 0) {
-                    f32x16 accp[4];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) accp[t] = f32x16{};
+            }
+            // ---- d P_band = G^T . q~ (target tile mt = segments 2mt, 2mt+1), fixed-point atomics ----
+            // in two passes of two channel tiles (32 accumulator registers instead of 64 beside accq)
+            if (2 * mt < nseg) {
+                for (int tp = 0; tp < 2; ++tp) {
+                    const int t0 = 2 * tp;
+                    if (t0 >= ntn) break;                            // uniform
+                    f32x16 accp[2] = {f32x16{}, f32x16{}};
+                    bf16x8 qh[2], ql[2];
+                    auto load_q = [&](int qs, int t) {
+                        const int cg = nt0 + min(t0 + t, ntn - 1);
+                        if constexpr (X3) {
+                            const int qrow = qy0 + (qs >> 1), qsx = (qx0 >> 4) + (qs & 1);
+                            const bool ok = qrow < g.H && qsx < g.qnsx;
+                            const __bf16* pp =
+                                a.qt + ((size_t)(b * g.QS + (ok ? qrow * g.qnsx + qsx : 0)) * ncg + cg) * unit + lane * 8;
+                            const bf16x8 z = {};
+                            qh[t] = ok ? *reinterpret_cast<const bf16x8*>(pp) : z;
+                            ql[t] = ok ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : z;
+                        } else {
+                            qh[t] = *reinterpret_cast<const bf16x8*>(qimg + ((size_t)(qs * ncg + cg) * 64 + lane) * 8);
+                            ql[t] = qh[t];
+                        }
+                    };
+                    load_q(0, 0);
+                    load_q(0, 1);
                     for (int ks = 0; ks < kBwdQ / 16; ++ks) {
-                        const int qrow = qy0 + (ks >> 1);
-                        if (qrow >= g.H) break;                      // uniform
                         float v[8];
 #pragma unroll
                         for (int e = 0; e < 8; ++e) v[e] = G[(ks * 16 + 8 * h + e) * kBwdLd + mt * 32 + j32];
                         bf16x8 ah, al;
                         split8(v, ah, al);
-                        const int qsx = (qx0 >> 4) + (ks & 1);
-                        if (qsx >= g.qnsx) continue;                 // uniform: a segment past the map's width
-                        const __bf16* qu = a.qt + ((size_t)(b * g.QS + qrow * g.qnsx + qsx) * ncg) * unit + lane * 8;
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if (t >= ntn) break;
-                            const __bf16* pp = qu + (size_t)(nt0 + t) * unit;
-                            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(pp);
-                            const bf16x8 bl = X3 ? *reinterpret_cast<const bf16x8*>(pp + 64 * 8) : bh;
-                            mma3<X3>(accp[t], ah, al, bh, bl);
+                        for (int t = 0; t < 2; ++t) {
+                            if (t0 + t < ntn) mma3<X3>(accp[t], ah, al, qh[t], ql[t]);
+                            load_q(min(ks + 1, kBwdQ / 16 - 1), t);
                         }
                     }
-                    // lane (channel j32, half h): register 4i + k is target column mt*32 + 8i + 4h + k
-                    double* drow = a.dP + ((size_t)b * a.pT + a.poff[l] + (size_t)ty * lw) * g.C;
+                    // lane (channel j32, half h): register 4i + k is band target mt*32 + 8i + 4h + k
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        if (t >= ntn) break;
-                        const int ch = (nt0 + t) * 32 + j32;
+                    for (int t = 0; t < 2; ++t) {
+                        const int ch = (nt0 + t0 + t) * 32 + j32;
+                        if (t0 + t >= ntn || ch >= g.C) continue;
 #pragma unroll
                         for (int v = 0; v < 16; ++v) {
-                            const int col = mt * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
-                            const int tx = cx + col;
-                            if (col < ncols && tx <= ext.y && ch < g.C &&
-                                (RMD_OTF_BWD_ABL == 0 || accp[t][v] == 1.2345e30f))      // ablation: no adds
-                                atomicAdd(drow + (size_t)tx * g.C + ch, (double)accp[t][v]);
+                            const int jt = mt * 32 + 8 * (v >> 2) + 4 * h + (v & 3);
+                            const int s = jt >> 4;
+                            if (s >= nseg) continue;
+                            const int tx = bseg_x[s] * 16 + (jt & 15);
+                            const float val = accp[t][v];
+                            if (tx >= lw || val == 0.f || RMD_OTF_BWD_ABL == 1) continue;
+                            const size_t e = ((size_t)b * a.pT + a.poff[l] + (size_t)bseg_row[s] * lw + tx) * g.C + ch;
+                            if (__builtin_isfinite(val))
+                                atomicAdd(reinterpret_cast<unsigned long long*>(a.dP + e),
+                                          (unsigned long long)(long long)__builtin_rint((double)val * fscale));
+                            else {
+                                atomicAdd(a.dPnf + e, val);
+                                *a.nf = 1;
+                            }
                         }
                     }
                 }
@@ -915,26 +1112,64 @@ otf_backward_kernel(BwdArgs a) {
     }
 }
 
-// d fmap2[b, c, y, x] = sum_l d P_l[b, (y >> l, x >> l), c] / 4^l over the floor-cropped part of each level
-// (the transpose of l successive 2x2 average pools); one thread per (b, y, x, c), channel fastest.
-__global__ void __launch_bounds__(kThreads)
-otf_unpool_kernel(const double* __restrict__ dP, OtfGeom g, long long pT, LevelOff po, float* __restrict__ gf2) {
-    const long long N = (long long)g.H * g.W;
-    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    if (idx >= (long long)g.B * N * g.C) return;
-    const int c = (int)(idx % g.C);
-    const long long p = (idx / g.C) % N;
-    const int b = (int)(idx / ((long long)g.C * N));
-    const int y = (int)(p / g.W), x = (int)(p % g.W);
-    float s = 0.f;
+// the largest recorded |weight| of up to 64 records (their kMaxSlots header words) -> *acc (one wave)
+__global__ void otf_wmax_kernel(BwdWmax wm, int n, unsigned* __restrict__ acc) {
+    unsigned m = 0;
+    for (int i = 0; i < n; ++i) m = max(m, wm.p[i][threadIdx.x]);
 #pragma unroll
-    for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
-        if (l >= g.L) break;
-        const int yy = y >> l, xx = x >> l;
-        if (yy < g.lh[l] && xx < g.lw[l])
-            s += (float)dP[((size_t)b * pT + po.o[l] + (size_t)yy * g.lw[l] + xx) * g.C + c] * (1.0f / (float)(1 << (2 * l)));
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if (threadIdx.x == 0) atomicMax(acc, m);
+}
+
+// the fixed-point exponent of this backward's d P from the maxima (one wave)
+__global__ void otf_fixed_exp_kernel(const unsigned* __restrict__ wmax, const unsigned* __restrict__ qmax, int nrec,
+                                     long long N, int* __restrict__ sexp) {
+    unsigned mq = qmax[threadIdx.x];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mq = max(mq, (unsigned)__shfl_xor((int)mq, o));
+    const float bound = (float)nrec * (float)N * __uint_as_float(*wmax) * __uint_as_float(mq);
+    if (threadIdx.x == 0) *sexp = fixed_exp(bound * 1.0001f);
+}
+
+// d fmap2[b, c, y, x] = sum_l d P_l[b, (y >> l, x >> l), c] / 4^l over the floor-cropped part of each level
+// (the transpose of l successive 2x2 average pools).  d P: fixed point in 2^-s units plus the
+// non-finite side buffer (read only when *nf is set).  A 256-thread block takes 64 pixels x 64
+// channels: reads run along the channels of d P's pixel-major rows, the transposed writes along the
+// pixels of the planar output (through an LDS tile).
+__global__ void __launch_bounds__(256)
+otf_unpool_kernel(const long long* __restrict__ dP, const float* __restrict__ dPnf, const int* __restrict__ sexp,
+                  const int* __restrict__ nf, OtfGeom g, long long pT, LevelOff po, float* __restrict__ gf2) {
+    __shared__ float tile[64][65];
+    const long long N = (long long)g.H * g.W;
+    const long long p0 = (long long)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64, b = blockIdx.z;
+    const double inv = ldexp(1.0, -*sexp);
+    const bool anynf = *nf != 0;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int px = i >> 6, c = c0 + (i & 63);
+        const long long p = p0 + px;
+        float s = 0.f;
+        if (p < N && c < g.C) {
+            const int y = (int)(p / g.W), x = (int)(p % g.W);
+#pragma unroll
+            for (int l = 0; l < RMD_MAX_LEVELS; ++l) {
+                if (l >= g.L) break;
+                const int yy = y >> l, xx = x >> l;
+                if (yy < g.lh[l] && xx < g.lw[l]) {
+                    const size_t e = ((size_t)b * pT + po.o[l] + (size_t)yy * g.lw[l] + xx) * g.C + c;
+                    const float v = (float)((double)dP[e] * inv) + (anynf ? dPnf[e] : 0.f);
+                    s += v * (1.0f / (float)(1 << (2 * l)));
+                }
+            }
+        }
+        tile[px][i & 63] = s;
     }
-    gf2[((size_t)b * g.C + c) * N + p] = s;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int c = c0 + (i >> 6), px = i & 63;
+        const long long p = p0 + px;
+        if (p < N && c < g.C) gf2[((size_t)b * g.C + c) * N + p] = tile[px][i >> 6];
+    }
 }
 
 int check_otf(int batch, int channels, int height, int width, int levels, int compute) {
@@ -1094,11 +1329,13 @@ namespace {
 
 struct BwdLayout {
     OtfGeom g, gq;              // targets (all levels) / queries (level 0 of fmap1)
-    size_t pt_off, qt_off, dp_off, total;
+    size_t pt_off, qt_off, dp_off, nf_off, sc_off, total;
     long long pT;
     long long poff[RMD_MAX_LEVELS];
 };
 
+// workspace: target T layout | query T layout | d P fixed point (int64) | d P non-finite (float) |
+// scalars (qmax, wmax, s)
 BwdLayout bwd_layout(int B, int C, int H, int W, int L, int compute) {
     BwdLayout y{};
     y.g = make_otf_geom(B, C, H, W, L);
@@ -1115,20 +1352,31 @@ BwdLayout bwd_layout(int B, int C, int H, int W, int L, int compute) {
         p += (long long)y.g.lh[l] * y.g.lw[l];
     }
     y.pT = p;
+    auto up = [](size_t v) { return (v + 255) / 256 * 256; };
     y.pt_off = 0;
-    y.qt_off = (tbytes + 255) / 256 * 256;
-    y.dp_off = y.qt_off + (qbytes + 255) / 256 * 256;
-    y.total = y.dp_off + (size_t)B * p * C * sizeof(double);
+    y.qt_off = up(tbytes);
+    y.dp_off = y.qt_off + up(qbytes);
+    y.nf_off = y.dp_off + up((size_t)B * p * C * sizeof(long long));
+    y.sc_off = y.nf_off + up((size_t)B * p * C * sizeof(float));
+    y.total = y.sc_off + 512;
     return y;
 }
+
+// LDS of otf_backward_kernel: dynamic (G, bf16 query image, per-row extents) + static (origins, box, band)
+size_t bwd_lds_dynamic(int ncg, bool x3, int height) {
+    return sizeof(float) * kBwdQ * kBwdLd + (x3 ? 0 : (size_t)8 * ncg * 1024) + sizeof(int2) * (size_t)height;
+}
+constexpr size_t kBwdLdsStatic = sizeof(int2) * kMaxRec * kBwdQ + sizeof(int) * (4 + 2 * kBwdSeg + 4 * kBwdRows + 4) +
+                                 2 * sizeof(void*) * kMaxRec;
 
 }  // namespace
 
 extern "C" size_t rmd_corr_otf_record_bytes(int batch, int height, int width, int levels, int radius) {
     if (batch <= 0 || height <= 0 || width <= 0 || levels < 1 || levels > RMD_MAX_LEVELS || radius < 1 || radius > 8)
         return 0;
-    const size_t K = 2 * radius + 2;
-    return otf_record_org_bytes(batch, height, width, levels) + (size_t)levels * batch * height * width * K * K * sizeof(float);
+    const int K = 2 * radius + 2;
+    // origins | weights | 256-B header (largest |weight|, for the fixed-point scale of the backward)
+    return otf_record_org_bytes(batch, height, width, levels) + otf_record_wp_bytes(batch, height, width, levels, K) + 256;
 }
 
 extern "C" int rmd_corr_otf_record(const float* grad_out, const float* coords, int batch, int height, int width,
@@ -1137,13 +1385,20 @@ extern "C" int rmd_corr_otf_record(const float* grad_out, const float* coords, i
     RMD_REQUIRE(rmd_corr_otf_record_bytes(batch, height, width, levels, radius) > 0, RMD_ERR_SHAPE,
                 "rmd_corr_otf_record: bad sizes or radius %d not in 1..8", radius);
     const OtfGeom g = make_otf_geom(batch, 1, height, width, levels);
+    const int K = 2 * radius + 2;
     int2* org = static_cast<int2*>(record);
-    float* wp = reinterpret_cast<float*>(static_cast<char*>(record) + otf_record_org_bytes(batch, height, width, levels));
+    char* base = static_cast<char*>(record) + otf_record_org_bytes(batch, height, width, levels);
+    float* wp = reinterpret_cast<float*>(base);
+    unsigned* wmax = reinterpret_cast<unsigned*>(base + otf_record_wp_bytes(batch, height, width, levels, K));
     const long long n = (long long)levels * batch * height * width;
     const unsigned blocks = (unsigned)((n + kThreads - 1) / kThreads);
     hipStream_t st = as_stream(stream);
+    if (hipMemsetAsync(wmax, 0, sizeof(unsigned) * kMaxSlots, st) != hipSuccess) {
+        set_error("rmd_corr_otf_record: hipMemsetAsync failed");
+        return RMD_ERR_LAUNCH;
+    }
     switch (radius) {
-#define RMD_CASE(RR) case RR: otf_record_kernel<RR><<<blocks, kThreads, 0, st>>>(grad_out, coords, g, zero_level_mask, org, wp); break;
+#define RMD_CASE(RR) case RR: otf_record_kernel<RR><<<blocks, kThreads, 0, st>>>(grad_out, coords, g, zero_level_mask, org, wp, wmax); break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE
     }
@@ -1166,16 +1421,31 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
     if (rc) return rc;
     RMD_REQUIRE(channels <= 256, RMD_ERR_SHAPE, "rmd_corr_otf_backward: channels %d > 256", channels);
     RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_otf_backward: radius %d not in 1..8", radius);
+    for (int i = 0; i < nrecords; ++i)
+        RMD_REQUIRE(records[i], RMD_ERR_ARG, "rmd_corr_otf_backward: null record %d", i);
     hipStream_t st = as_stream(stream);
     const BwdLayout y = bwd_layout(batch, channels, height, width, levels, compute);
     const bool x3 = compute != RMD_BF16;
+    const int ncg = y.g.Cp / 32;
+    // LDS per block (dynamic + static) against the 160 KiB of a CU, checked before any launch
+    const size_t lds = bwd_lds_dynamic(ncg, x3, height);
+    RMD_REQUIRE(lds + kBwdLdsStatic <= 160 * 1024, RMD_ERR_SHAPE,
+                "rmd_corr_otf_backward: a %d-row map needs %zu B of LDS per block (dynamic %zu + static %zu) > 160 KiB",
+                height, lds + kBwdLdsStatic, lds, kBwdLdsStatic);
     char* ws = static_cast<char*>(workspace);
     __bf16* pt = reinterpret_cast<__bf16*>(ws + y.pt_off);
     __bf16* qt = reinterpret_cast<__bf16*>(ws + y.qt_off);
-    double* dP = reinterpret_cast<double*>(ws + y.dp_off);
+    long long* dP = reinterpret_cast<long long*>(ws + y.dp_off);
+    float* dPnf = reinterpret_cast<float*>(ws + y.nf_off);
+    unsigned* qmax = reinterpret_cast<unsigned*>(ws + y.sc_off);     // kMaxSlots partial maxima
+    unsigned* wmax = qmax + kMaxSlots;
+    int* sexp = reinterpret_cast<int*>(qmax + kMaxSlots + 1);
+    int* nf = sexp + 1;
     const size_t N = (size_t)height * width;
     if (hipMemsetAsync(grad_fmap1, 0, (size_t)batch * channels * N * sizeof(float), st) != hipSuccess ||
-        hipMemsetAsync(dP, 0, (size_t)batch * y.pT * channels * sizeof(double), st) != hipSuccess) {
+        hipMemsetAsync(dP, 0, (size_t)batch * y.pT * channels * sizeof(long long), st) != hipSuccess ||
+        hipMemsetAsync(dPnf, 0, (size_t)batch * y.pT * channels * sizeof(float), st) != hipSuccess ||
+        hipMemsetAsync(qmax, 0, 512, st) != hipSuccess) {
         set_error("rmd_corr_otf_backward: hipMemsetAsync failed");
         return RMD_ERR_LAUNCH;
     }
@@ -1195,40 +1465,52 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
         const long long nt = (long long)batch * y.g.TS * (y.g.Cp / 32) * 64;
         const long long nq = (long long)batch * y.gq.TS * (y.gq.Cp / 32) * 64;
         if (x3) {
-            otf_tlayout_kernel<true><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt);
-            otf_tlayout_kernel<true><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt);
+            otf_tlayout_kernel<true><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt, nullptr);
+            otf_tlayout_kernel<true><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt, qmax);
         } else {
-            otf_tlayout_kernel<false><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt);
-            otf_tlayout_kernel<false><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt);
+            otf_tlayout_kernel<false><<<(unsigned)((nt + kThreads - 1) / kThreads), kThreads, 0, st>>>(lt, y.g, 1.0f, pt, nullptr);
+            otf_tlayout_kernel<false><<<(unsigned)((nq + kThreads - 1) / kThreads), kThreads, 0, st>>>(lq, y.gq, scale, qt, qmax);
         }
         rc = check_launch("rmd_corr_otf_backward (operands)");
         if (rc) return rc;
     }
+    // fixed-point exponent of d P from the largest recorded |weight| and |q~|
+    const size_t obytes = otf_record_org_bytes(batch, height, width, levels);
+    const size_t wbytes = otf_record_wp_bytes(batch, height, width, levels, 2 * radius + 2);
+    for (int r0 = 0; r0 < nrecords; r0 += 64) {
+        BwdWmax wm{};
+        const int n = std::min(64, nrecords - r0);
+        for (int i = 0; i < n; ++i)
+            wm.p[i] = reinterpret_cast<const unsigned*>(static_cast<const char*>(records[r0 + i]) + obytes + wbytes);
+        otf_wmax_kernel<<<1, kMaxSlots, 0, st>>>(wm, n, wmax);
+    }
+    otf_fixed_exp_kernel<<<1, kMaxSlots, 0, st>>>(wmax, qmax, std::max(nrecords, 1), (long long)N, sexp);
+    rc = check_launch("rmd_corr_otf_backward (scale)");
+    if (rc) return rc;
     const long long nblk = (long long)((width + kBwdQX - 1) / kBwdQX) * ((height + kBwdQY - 1) / kBwdQY) * batch;
     RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_backward: grid too large");
-    const size_t lds = sizeof(float) * kBwdQ * kBwdLd + sizeof(int2) * height;     // G + per-row extents
-    const size_t obytes = otf_record_org_bytes(batch, height, width, levels);
     for (int r0 = 0; r0 < nrecords; r0 += kMaxRec) {
         BwdArgs a{};
         a.g = y.g;
         a.pt = pt;
         a.qt = qt;
         a.dP = dP;
+        a.dPnf = dPnf;
         a.pT = y.pT;
         for (int l = 0; l < RMD_MAX_LEVELS; ++l) a.poff[l] = y.poff[l];
         a.gq = grad_fmap1;
         a.scale = scale;
+        a.sexp = sexp;
+        a.nf = nf;
         a.rec.n = std::min(kMaxRec, nrecords - r0);
         for (int i = 0; i < a.rec.n; ++i) {
-            RMD_REQUIRE(records[r0 + i], RMD_ERR_ARG, "rmd_corr_otf_backward: null record %d", r0 + i);
             a.rec.org[i] = static_cast<const int2*>(records[r0 + i]);
             a.rec.wp[i] = reinterpret_cast<const float*>(static_cast<const char*>(records[r0 + i]) + obytes);
         }
 #define RMD_BWD(XX, RR)                                                                                          \
         do {                                                                                                     \
             auto k = otf_backward_kernel<XX, RR>;                                                                \
-            RMD_REQUIRE(lds <= 160 * 1024, RMD_ERR_SHAPE, "rmd_corr_otf_backward: %zu B of LDS per block", lds);    \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
                                       (int)lds);                                                                 \
             k<<<(unsigned)nblk, kBwdThreads, lds, st>>>(a);                                                      \
         } while (0)
@@ -1251,7 +1533,7 @@ extern "C" int rmd_corr_otf_backward(const float* fmap1, const float* fmap2, con
     }
     LevelOff po{};
     for (int l = 0; l < RMD_MAX_LEVELS; ++l) po.o[l] = y.poff[l];
-    const long long n2 = (long long)batch * N * channels;
-    otf_unpool_kernel<<<(unsigned)((n2 + kThreads - 1) / kThreads), kThreads, 0, st>>>(dP, y.g, y.pT, po, grad_fmap2);
+    const dim3 ugrid((unsigned)((N + 63) / 64), (unsigned)((channels + 63) / 64), (unsigned)batch);
+    otf_unpool_kernel<<<ugrid, 256, 0, st>>>(dP, dPnf, sexp, nf, y.g, y.pT, po, grad_fmap2);
     return check_launch("rmd_corr_otf_backward (unpool)");
 }

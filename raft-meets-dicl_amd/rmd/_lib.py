@@ -66,7 +66,7 @@ _SIGS = {
     "rmd_corr_pool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_corr_unpool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_corr_grad_gemm_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I]),
-    "rmd_corr_grad_gemm": (_I, [_P, ctypes.c_longlong, _P, ctypes.c_longlong, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "rmd_corr_grad_gemm": (_I, [_P, ctypes.c_longlong, _P, ctypes.c_longlong, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rmd_dicl_stack": (_I, [_P, _P, _P] + [_I] * 11 + [_P, _P]),
     "rmd_dicl_stack_backward": (_I, [_P, _P] + [_I] * 11 + [_P, _P, _P]),
     "rmd_dicl_stack_int_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I]),

@@ -276,9 +276,10 @@ def otf_lookup_autograd(token, state, coords, radius, mask_costs=()):
 # input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
 # accumulates into ONE dense fp32 gradient G over the T' padded targets, in the pyramid's chunked
 # query-minor order (8-target chunks, include/rmd.h, rmd_corr_lookup_backward), shared through
-# _CorrState; the pyramid backward then turns G into d fmap1 / d fmap2 with two split-bf16 MFMA GEMMs
-# that read G in its blocked order (rmd_corr_grad_gemm layouts 3 / 2, no transpose pass) and the
-# native pool / unpool kernels (backward in fp32 in every precision mode).
+# _CorrState; the pyramid backward then turns G into d fmap1 / d fmap2 with two MFMA GEMMs that read G
+# in its blocked order (rmd_corr_grad_gemm layouts 3 / 2, no transpose pass; split-bf16 products in the
+# fp32 modes, bf16 products with fp32 accumulation in the bf16 modes) and the native pool / unpool
+# kernels (G, pool and unpool in fp32 in every mode).
 
 class _CorrState:
     def __init__(self, pyr, f1, f2, precision):
@@ -330,10 +331,12 @@ class _CorrPyramidFn(torch.autograd.Function):
                                  lib.rmd_corr_grad_gemm_workspace_bytes(b, c, n, t), 1),
                              dtype=torch.uint8, device=f1.device)
             # grad_fmap1 = P G (K = T', layout 3: G blocked along k), dP = fmap1 G^T (K = N, layout 2: G
-            # blocked along n): split-bf16 MFMA GEMMs (corr_grad.hip)
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, _ptr(g1), _ptr(ws),
+            # blocked along n): MFMA GEMMs (corr_grad.hip) in the block's compute — split-bf16 (fp32
+            # accuracy) for the fp32 modes, one bf16 product for the bf16 modes
+            gc = RMD_BF16 if PRECISIONS[st.precision][0] == RMD_BF16 else RMD_BF16X3
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, gc, _ptr(g1), _ptr(ws),
                                               stream), "rmd_corr_grad_gemm")
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, _ptr(dpool), _ptr(ws),
+            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, gc, _ptr(dpool), _ptr(ws),
                                               stream), "rmd_corr_grad_gemm")
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")

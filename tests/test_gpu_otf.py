@@ -243,6 +243,55 @@ def test_otf_backward_is_deterministic(precision):
         assert np.array_equal(g1, runs[0][0]) and np.array_equal(g2, runs[0][1])
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_otf_backward_deterministic_across_wide_dynamic_range(precision):
+    """d P contributions whose magnitudes span far more than 2^29 (upstream gradients
+    scaled per query by 2^-40 .. 2^+8, so a pooled target sums terms ~2^48 apart) stay run-to-run bitwise
+    equal (64-bit fixed-point accumulation is associative) and match the float64 oracle."""
+    import rmd
+    rng = np.random.default_rng(5)
+    b, c, h, w, levels, r = 1, 32, 24, 40, 3, 3
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    cos = [_grid_coords(rng, b, h, w, 1.5) for _ in range(4)]
+    d = (2 * r + 1) ** 2
+    mag = np.exp2(rng.integers(-40, 9, size=(b, 1, h, w))).astype(np.float32)
+    gos = [(rng.standard_normal((b, levels * d, h, w)) * mag).astype(np.float32) for _ in range(4)]
+    runs = [_grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, levels, r, precision=precision, method="otf"),
+                   f1, f2, cos, gos)[1:] for _ in range(3)]
+    for g1, g2 in runs[1:]:
+        assert np.array_equal(g1, runs[0][0]) and np.array_equal(g2, runs[0][1])
+    r1 = np.zeros(f1.shape)
+    r2 = np.zeros(f2.shape)
+    for co, go in zip(cos, gos):
+        a1, a2 = oracle.corr_lookup_fs_backward(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64),
+                                                levels, r, go.astype(np.float64), ())
+        r1 += a1
+        r2 += a2
+    assert rel_max_err(runs[0][0], r1) < TOL[precision]
+    assert rel_max_err(runs[0][1], r2) < TOL[precision]
+
+
+def test_otf_backward_propagates_non_finite_gradients():
+    """A NaN in the upstream gradient reaches the pooled-target gradient (through the float side buffer
+    of the fixed-point accumulation) as it does through the reference's autograd; finite inputs stay
+    finite."""
+    import rmd
+    rng = np.random.default_rng(8)
+    b, c, h, w = 1, 16, 12, 20
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    co = _grid_coords(rng, b, h, w, 0.5)
+    go = rng.standard_normal((b, 2 * 25, h, w)).astype(np.float32)
+    _, g1, g2 = _grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, 2, 2, precision="fp32", method="otf"), f1, f2, [co],
+                       [go])
+    assert np.isfinite(g1).all() and np.isfinite(g2).all()
+    go[0, 12, 5, 7] = np.nan
+    _, g1, g2 = _grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, 2, 2, precision="fp32", method="otf"), f1, f2, [co],
+                       [go])
+    assert np.isnan(g2).any() and np.isnan(g1).any()
+
+
 def test_otf_backward_equals_volume_backward_raft_scale():
     """rmd.raft.CorrBlock (scale 1/sqrt(C)) trained through the on-the-fly path gives the volume path's
     gradients (fp32 mode, 12 lookups with a flow that moves every iteration, B=2 at the cfg2 map size)."""
