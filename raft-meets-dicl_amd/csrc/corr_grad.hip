@@ -34,10 +34,11 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-constexpr int kTM = 256, kTN = 128, kKC = 32;
+constexpr int kTM = 256, kKC = 32;
 constexpr int kRowB = 144;                                  // hi 64 B | lo 64 B | pad 16 B (9 x 16 B: odd)
-constexpr int kLdsA = kTM * kRowB, kLdsB = kTN * kRowB;     // 36,864 + 18,432 B per buffer
-constexpr int kLdsBuf = kLdsA + kLdsB;                      // one buffer: 55,296 B (two: 110,592 B)
+constexpr int kLdsA = kTM * kRowB;                          // 36,864 B per buffer
+// output tile kTM x TN: TN = 128 (two buffers 110,592 B of LDS) or 256 (147,456 B: A re-read half as often)
+template <int TN> constexpr int lds_buf() { return kLdsA + TN * kRowB; }
 
 struct GemmArgs {
     const float* A;
@@ -84,9 +85,11 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ at, int k, int
 // of the next chunk runs beside the current chunk's MFMAs (waves 0-3 and 4-7 share each SIMD).
 // X3 = false (compute RMD_BF16, the bf16 precision mode): one bf16 product per k-step (hi.hi), the lo
 // halves are neither split nor stored
-template <bool VA, bool VB, int LAYOUT, bool X3 = true>
+template <bool VA, bool VB, int LAYOUT, bool X3 = true, int TN = 128>
 __global__ void __launch_bounds__(512, 1)
 grad_gemm_x3(GemmArgs p) {
+    constexpr int kTN = TN, kLdsBuf = lds_buf<TN>();
+    constexpr int NJ = TN / 64;                 // 32-column MFMA tiles per wave (a wave owns 64 x TN/2)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nwg = gridDim.x;
     int id = xcd_block(blockIdx.x, nwg);       // consecutive ids (same batch, same A rows) share an XCD
@@ -104,8 +107,8 @@ grad_gemm_x3(GemmArgs p) {
     const float* __restrict__ A = p.A + (size_t)b * p.sa;
     const float* __restrict__ Bm = p.Bm + (size_t)b * p.sb;
 
-    // per thread: A 4 x float4 (rows m0 + 64 it + tid / 8, k 4 (tid % 8) .. +3); B 2 x float4
-    float4 ra[4], rb[2];
+    // per thread: A 4 x float4 (rows m0 + 64 it + tid / 8, k 4 (tid % 8) .. +3); B TN / 64 x float4
+    float4 ra[4], rb[TN / 64];
     auto gload = [&](int k0) {
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
@@ -116,27 +119,32 @@ grad_gemm_x3(GemmArgs p) {
             // thread (kq, nq): k rows 2kq, 2kq + 1 of columns 4nq .. 4nq + 3 (16 kq per 16 lanes of a
             // wave group: lanes (kq & 15, n) read 2 k rows x 64 contiguous bytes; waves 0-3 / 4-7 take
             // column halves 0-63 / 64-127; layout 2: 4 consecutive n of one 8-block are contiguous too)
-            const int kq = (lane & 3) | ((w & 3) << 2), n = n0 + 64 * (w >> 2) + 4 * (lane >> 2);
+            const int kq = (lane & 3) | ((w & 3) << 2);
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int k = k0 + 2 * kq + r;
-                rb[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (k < ke) {
-                    const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb + n
-                                                   : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
-                    if (VB && n + 3 < p.Nc) {
-                        rb[r] = *reinterpret_cast<const float4*>(src);
-                    } else {
-                        rb[r].x = n + 0 < p.Nc ? src[0] : 0.f;
-                        rb[r].y = n + 1 < p.Nc ? src[1] : 0.f;
-                        rb[r].z = n + 2 < p.Nc ? src[2] : 0.f;
-                        rb[r].w = n + 3 < p.Nc ? src[3] : 0.f;
+            for (int nn = 0; nn < TN / 128; ++nn) {
+                const int n = n0 + (TN / 2) * (w >> 2) + 64 * nn + 4 * (lane >> 2);
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int k = k0 + 2 * kq + r;
+                    float4& d = rb[2 * nn + r];
+                    d = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (k < ke) {
+                        const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb + n
+                                                       : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
+                        if (VB && n + 3 < p.Nc) {
+                            d = *reinterpret_cast<const float4*>(src);
+                        } else {
+                            d.x = n + 0 < p.Nc ? src[0] : 0.f;
+                            d.y = n + 1 < p.Nc ? src[1] : 0.f;
+                            d.z = n + 2 < p.Nc ? src[2] : 0.f;
+                            d.w = n + 3 < p.Nc ? src[3] : 0.f;
+                        }
                     }
                 }
             }
         } else {
 #pragma unroll
-            for (int it = 0; it < 2; ++it) {
+            for (int it = 0; it < TN / 64; ++it) {
                 const int row = n0 + it * 64 + (tid >> 3), k = k0 + (tid & 7) * 4;
                 // layout 3: k .. k + 3 lie in one 8-block (k % 4 == 0), contiguous like layout 1's row
                 const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb + k
@@ -158,22 +166,27 @@ grad_gemm_x3(GemmArgs p) {
         }
         if constexpr (LAYOUT == 0 || LAYOUT == 2) {
             // transpose: column 4nq + j of the thread's 2 k rows -> LDS row of that column, k offset 2kq
-            const int kq = (lane & 3) | ((w & 3) << 2), nr = 64 * (w >> 2) + 4 * (lane >> 2);
-            const float c0[2] = {rb[0].x, rb[1].x}, c1[2] = {rb[0].y, rb[1].y};
-            const float c2[2] = {rb[0].z, rb[1].z}, c3[2] = {rb[0].w, rb[1].w};
-            const float* cols[4] = {c0, c1, c2, c3};
+            const int kq = (lane & 3) | ((w & 3) << 2);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                __bf16 h0 = (__bf16)cols[j][0], h1 = (__bf16)cols[j][1];
-                __bf16 l0 = (__bf16)(cols[j][0] - (float)h0), l1 = (__bf16)(cols[j][1] - (float)h1);
-                typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-                unsigned char* d = sB + (nr + j) * kRowB + kq * 4;
-                *reinterpret_cast<bf16x2*>(d) = bf16x2{h0, h1};
-                if constexpr (X3) *reinterpret_cast<bf16x2*>(d + 64) = bf16x2{l0, l1};
+            for (int nn = 0; nn < TN / 128; ++nn) {
+                const int nr = (TN / 2) * (w >> 2) + 64 * nn + 4 * (lane >> 2);
+                const float4 r0 = rb[2 * nn], r1 = rb[2 * nn + 1];
+                const float c0[2] = {r0.x, r1.x}, c1[2] = {r0.y, r1.y};
+                const float c2[2] = {r0.z, r1.z}, c3[2] = {r0.w, r1.w};
+                const float* cols[4] = {c0, c1, c2, c3};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    __bf16 h0 = (__bf16)cols[j][0], h1 = (__bf16)cols[j][1];
+                    __bf16 l0 = (__bf16)(cols[j][0] - (float)h0), l1 = (__bf16)(cols[j][1] - (float)h1);
+                    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+                    unsigned char* d = sB + (nr + j) * kRowB + kq * 4;
+                    *reinterpret_cast<bf16x2*>(d) = bf16x2{h0, h1};
+                    if constexpr (X3) *reinterpret_cast<bf16x2*>(d + 64) = bf16x2{l0, l1};
+                }
             }
         } else {
 #pragma unroll
-            for (int it = 0; it < 2; ++it) {
+            for (int it = 0; it < TN / 64; ++it) {
                 bf16x4 hi, lo;
                 split4(rb[it].x, rb[it].y, rb[it].z, rb[it].w, hi, lo);
                 unsigned char* d = sB + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
@@ -183,15 +196,15 @@ grad_gemm_x3(GemmArgs p) {
         }
     };
 
-    f32x16 acc[2][2];
+    f32x16 acc[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{};
 
     const int j32 = lane & 31, h = lane >> 5;
     const unsigned aoff = (unsigned)((wm * 64 + j32) * kRowB + h * 16);
-    const unsigned boff = (unsigned)(kLdsA + (wn * 64 + j32) * kRowB + h * 16);
+    const unsigned boff = (unsigned)(kLdsA + (wn * (TN / 2) + j32) * kRowB + h * 16);
     const int nchunk = (ke - kb + kKC - 1) / kKC;
 
     // prologue: chunk 0 -> buffer 0, chunk 1 in flight in registers
@@ -207,22 +220,23 @@ grad_gemm_x3(GemmArgs p) {
         }
 #pragma unroll
         for (int s = 0; s < kKC / 16; ++s) {
-            bf16x8 ah[2], al[2], bh[2], bl[2];
+            bf16x8 ah[2], al[2], bh[NJ], bl[NJ];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const unsigned char* pa = cur + aoff + i * 32 * kRowB + s * 32;
-                const unsigned char* pb = cur + boff + i * 32 * kRowB + s * 32;
                 ah[i] = *reinterpret_cast<const bf16x8*>(pa);
-                bh[i] = *reinterpret_cast<const bf16x8*>(pb);
-                if constexpr (X3) {
-                    al[i] = *reinterpret_cast<const bf16x8*>(pa + 64);
-                    bl[i] = *reinterpret_cast<const bf16x8*>(pb + 64);
-                }
+                if constexpr (X3) al[i] = *reinterpret_cast<const bf16x8*>(pa + 64);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const unsigned char* pb = cur + boff + j * 32 * kRowB + s * 32;
+                bh[j] = *reinterpret_cast<const bf16x8*>(pb);
+                if constexpr (X3) bl[j] = *reinterpret_cast<const bf16x8*>(pb + 64);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int j = 0; j < NJ; ++j) {
                     f32x16 t = acc[i][j];
                     if constexpr (X3) {
                         t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], t, 0, 0, 0);
@@ -239,8 +253,8 @@ grad_gemm_x3(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn * 64 + j * 32 + j32;
+        for (int j = 0; j < NJ; ++j) {
+            const int col = n0 + wn * (TN / 2) + j * 32 + j32;
             if (col >= p.Nc) continue;
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
@@ -276,15 +290,23 @@ grad_gemm_reduce(const float* __restrict__ ws, long long n, int splits, float* _
 }
 
 struct Plan {
-    int ntm, ntn, splits, kper;
+    int ntm, ntn, splits, kper, tn;
 };
+
+// output-tile width: 256 columns (A operand re-read half as often through L2) once the matrix is wide
+// enough, else 128
+#ifndef RMD_GG_TN
+#define RMD_GG_TN 256
+#endif
+inline int tile_n(int Nc) { return RMD_GG_TN == 256 && Nc >= 1024 ? 256 : 128; }
 
 // split count: smallest s minimising (workgroup rounds over 256 CUs) x (K chunks per split), plus a
 // small charge per split for the workspace pass
 Plan plan(int batch, int M, int K, int Nc) {
     Plan pl{};
+    pl.tn = tile_n(Nc);
     pl.ntm = (M + kTM - 1) / kTM;
-    pl.ntn = (Nc + kTN - 1) / kTN;
+    pl.ntn = (Nc + pl.tn - 1) / pl.tn;
     const long long tiles = (long long)pl.ntm * pl.ntn * batch;
     const int nch = (K + kKC - 1) / kKC;
     double best = 1e30;
@@ -304,14 +326,20 @@ Plan plan(int batch, int M, int K, int Nc) {
     return pl;
 }
 
-template <bool VA, bool VB, int LAYOUT>
-void launch_gemm(const GemmArgs& a, int nwg, bool x3, hipStream_t st) {
-    auto k = x3 ? grad_gemm_x3<VA, VB, LAYOUT, true> : grad_gemm_x3<VA, VB, LAYOUT, false>;
+template <bool VA, bool VB, int LAYOUT, int TN>
+void launch_gemm_tn(const GemmArgs& a, int nwg, bool x3, hipStream_t st) {
+    auto k = x3 ? grad_gemm_x3<VA, VB, LAYOUT, true, TN> : grad_gemm_x3<VA, VB, LAYOUT, false, TN>;
     // the >64 KB LDS opt-in is per device: set it before every launch (cheap host call), so a process
     // that launches on a second GPU gets it too
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * kLdsBuf);
-    k<<<nwg, 512, 2 * kLdsBuf, st>>>(a);
+                              2 * lds_buf<TN>());
+    k<<<nwg, 512, 2 * lds_buf<TN>(), st>>>(a);
+}
+
+template <bool VA, bool VB, int LAYOUT>
+void launch_gemm(const GemmArgs& a, int nwg, bool x3, int tn, hipStream_t st) {
+    if (tn == 256) launch_gemm_tn<VA, VB, LAYOUT, 256>(a, nwg, x3, st);
+    else launch_gemm_tn<VA, VB, LAYOUT, 128>(a, nwg, x3, st);
 }
 
 }  // namespace
@@ -367,10 +395,10 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     const bool va = a16 && (lda & 3) == 0;
     bool vb = b16 && (ldb & 3) == 0;
 #define RMD_GG(VA, VB)                                                                      \
-    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, x3, st)                         \
-     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, x3, st)                       \
-     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, x3, st)                       \
-                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, x3, st))
+    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, x3, pl.tn, st)                  \
+     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, x3, pl.tn, st)                \
+     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, x3, pl.tn, st)                \
+                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, x3, pl.tn, st))
     if (layout >= 2) vb = b16;                 // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
     if (va && vb) RMD_GG(true, true);
     else if (va) RMD_GG(true, false);

@@ -52,12 +52,21 @@ def main():
         cb = rmd.raft.CorrBlock(f1.detach(), f2.detach(), 4, 4, precision=prec)
         return [cb(coords[i]) for i in range(12)]
 
+    def fwd_outs():
+        cb = rmd.raft.CorrBlock(f1, f2, 4, 4, precision=prec)
+        return [cb(coords[i]) for i in range(12)]
+
     with torch.no_grad():
         t_f = run(fwd_only, reps)
     t_fb = run(lambda: torch.autograd.grad(fwd(), (f1, f2)), reps)
+    # the same backward driven by the 12 upstream gradients directly (no torch loss multiply / sum /
+    # their backward): the correlation block's own backward kernels
+    t_fb2 = run(lambda: torch.autograd.grad(fwd_outs(), (f1, f2), gos), reps)
     print(json.dumps({"shape": f"B{b} C{c} {h}x{w}, 12 lookups", "precision": prec, "forward_ms": t_f,
                       "forward_backward_ms": t_fb, "backward_ms": t_fb - t_f,
-                      "note": "forward_backward includes the loss multiply-adds (torch)"}))
+                      "backward_ms_from_grad_out": t_fb2 - t_f,
+                      "note": "backward_ms: forward_backward includes the loss multiply-adds (torch); "
+                              "backward_ms_from_grad_out: autograd.grad(outputs, inputs, grad_outputs)"}))
 
 
 if __name__ == "__main__":
