@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--radius", type=int, default=4)
     ap.add_argument("--levels", type=int, default=4)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32-exact", "bf16-f32", "fp32-f16"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32-f32", "fp32-exact", "bf16-f32", "fp32-f16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
     ap.add_argument("--event-every", type=int, default=5,
@@ -756,13 +756,22 @@ def stored_traffic(precision):
     return {}, "none"
 
 
+def storage_bytes(precision):
+    """Bytes per stored pyramid element of a precision mode (fp32: RMD_S24, 3 bytes)."""
+    from rmd import _lib, ops
+    return {_lib.RMD_F32: 4, _lib.RMD_F16: 2, _lib.RMD_S24: 3}[ops.PRECISIONS[precision][1]]
+
+
+STORAGE_NAME = {4: "fp32", 3: "s24 (fp32 rounded to 16 significant bits)", 2: "fp16"}
+
+
 def rooflines(args, precision, B, h8, w8, gemm_ms, look_ms, traffic, traffic_note, n_gemm, n_look):
     """roofline dicts of the GEMM and of the lookup from their average launch times (algorithmic bytes /
     flops per launch) and the counter traffic."""
     from rmd import _lib, ops
     N = h8 * w8
     D = (2 * args.radius + 1) ** 2
-    s = 2 if precision in ("bf16", "fp32-f16") else 4
+    s = storage_bytes(precision)
     compute_dt = "fp32" if precision.startswith("fp32") else "bf16"
     levels = [(h8 >> i, w8 >> i) for i in range(args.levels)]
     look_bytes = B * N * (args.levels * (2 * args.radius + 2) ** 2 * s + args.levels * D * 4 + 8)
@@ -770,7 +779,7 @@ def rooflines(args, precision, B, h8, w8, gemm_ms, look_ms, traffic, traffic_not
     gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
     gemm_flop = 2.0 * B * N * N * args.channels
     # MFMA work actually issued: the fp32 mode runs three bf16 products per k-step (x3 kernel)
-    mfma_dt, mfma_mult = ("bf16", 3.0) if precision == "fp32" else (compute_dt, 1.0)
+    mfma_dt, mfma_mult = ("bf16", 3.0) if precision in ("fp32", "fp32-f32") else (compute_dt, 1.0)
     look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
@@ -832,7 +841,7 @@ def main():
     inputs = None if args.dry_run else rank_inputs(args, rank, world, h8, w8, device)
     elapsed, ev_gemm, ev_look = corr_leg(args, args.precision, inputs, world, device, args.steps, args.warmup)
 
-    s = 2 if args.precision in ("bf16", "fp32-f16") else 4
+    s = storage_bytes(args.precision)
     compute_dt = "fp32" if args.precision.startswith("fp32") else "bf16"
     res = {
         "metric": "frame-pairs/s @436x1024 RAFT 12 iters (1-8 GPU); corr MFMA% + lookup HBM%",
@@ -852,7 +861,7 @@ def main():
                    "image": f"{args.height}x{args.width} padded {H}x{W}", "feature_map": f"{h8}x{w8}",
                    "channels": args.channels, "batch_per_gpu": B, "global_batch": B * world,
                    "lookups_per_step": args.iters, "precision": args.precision,
-                   "pyramid_storage": "fp16" if s == 2 else "fp32", "parallelism": f"batch-shard x{world}"},
+                   "pyramid_storage": STORAGE_NAME[s], "parallelism": f"batch-shard x{world}"},
     }
     if args.dry_run:
         res["dry_run"] = "launcher / collective plumbing only: no GPU work, value meaningless"
@@ -874,7 +883,7 @@ def main():
         res["roofline_lookup"] = roof_look
         progress(rank, "headline leg done")
         if args.fp32_mode == "on" and args.precision != "fp32":
-            # the parity mode (north_star's fp32 gate) on the same inputs: x3 GEMM + fp32 pyramid
+            # the parity mode (north_star's fp32 gate) on the same inputs: x3 GEMM + 24-bit pyramid
             progress(rank, "fp32_mode leg")
             el32, eg32, el32l = corr_leg(args, "fp32", inputs, world, device, args.fp32_steps, 3)
             tr32, n32 = live_traffic(args, "fp32", B, rank, device) if live else (None, "")
@@ -887,7 +896,7 @@ def main():
                 res["fp32_mode"] = {"value": world * B * args.fp32_steps / el32, "unit": "frame-pairs/s",
                                     "ms_per_step": el32 / args.fp32_steps * 1e3, "steps": args.fp32_steps,
                                     "warmup": 3, "precision": "fp32", "dtype": "fp32",
-                                    "pyramid_storage": "fp32",
+                                    "pyramid_storage": STORAGE_NAME[storage_bytes("fp32")],
                                     "gemm": "split-bf16 x3 MFMA (hi.hi + hi.lo + lo.hi), fp32 accumulate",
                                     "roofline_gemm": g32, "roofline_lookup": l32}
         del inputs

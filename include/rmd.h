@@ -38,6 +38,9 @@ extern "C" {
 #define RMD_F16 1
 #define RMD_BF16 2
 #define RMD_BF16X3 3   /* compute only: fp32-accurate split bf16, hi.hi + hi.lo + lo.hi per k-step */
+#define RMD_S24 4      /* storage only: an fp32 value rounded to its top 24 bits (sign, exponent, 15 mantissa
+                          bits; round half away from zero, NaN stays NaN), stored as 3 little-endian bytes
+                          (bytes 1..3 of the float); row layout only, written by the x3 GEMM */
 
 #define RMD_MAX_LEVELS 4
 
@@ -74,7 +77,7 @@ extern "C" {
 typedef struct rmd_pyramid_desc {
     int batch, height, width;          /* query grid == level-0 target grid                  */
     int levels;                        /* 1 .. RMD_MAX_LEVELS                                */
-    int storage;                       /* RMD_F32 or RMD_F16                                 */
+    int storage;                       /* RMD_F32, RMD_F16 or RMD_S24 (3 bytes per element)   */
     int level_h[RMD_MAX_LEVELS], level_w[RMD_MAX_LEVELS];
     int tile_h[RMD_MAX_LEVELS], tile_w[RMD_MAX_LEVELS];
     int tiles_y[RMD_MAX_LEVELS], tiles_x[RMD_MAX_LEVELS];

@@ -32,8 +32,8 @@ extern "C" int rmd_pyramid_describe_layout(int batch, int height, int width, int
         rmd::set_error("rmd_pyramid_describe: null desc");
         return RMD_ERR_ARG;
     }
-    if (storage != RMD_F32 && storage != RMD_F16) {
-        rmd::set_error("rmd_pyramid_describe: storage must be RMD_F32 or RMD_F16");
+    if (storage != RMD_F32 && storage != RMD_F16 && storage != RMD_S24) {
+        rmd::set_error("rmd_pyramid_describe: storage must be RMD_F32, RMD_F16 or RMD_S24");
         return RMD_ERR_ARG;
     }
     if (layout != RMD_LAYOUT_ROWS && !(layout == RMD_LAYOUT_TILES && storage == RMD_F16)) {

@@ -18,6 +18,8 @@
 //    lane loads 2-3 chunk rows of 3-4 quads and picks each patch row's half-chunks by the parity of
 //    its first patch row.
 
+#include <type_traits>
+
 #include "rmd_common.h"
 
 namespace rmd {
@@ -119,10 +121,22 @@ constexpr unsigned kOOB = 0x80000000u;
 __device__ unsigned g_abl_off = 0x80000000u;
 #endif
 
+// RMD_S24 storage element (include/rmd.h): bytes 1..3 of an fp32 word, little endian
+struct s24_t {
+    unsigned char b[3];
+};
+template <typename T> constexpr bool kIsS24 = false;
+template <> constexpr bool kIsS24<s24_t> = true;
+
+template <typename T>
+__device__ __forceinline__ const T* level_base(const T* pyr, const PyrGeom& g, int L, int b) {
+    return pyr + g.off[L] + (long long)b * ((long long)g.ty[L] * g.tx[L] * g.slots * g.th[L] * g.tw[L]);
+}
+
 template <typename T>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t level_rsrc(const T* pyr, const PyrGeom& g, int L, int b) {
     const long long per = (long long)g.ty[L] * g.tx[L] * g.slots * g.th[L] * g.tw[L];     // elements per image
-    const T* base = pyr + g.off[L] + (long long)b * per;
+    const T* base = level_base(pyr, g, L, b);
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0,
@@ -152,6 +166,34 @@ __device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_r
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * k), 0, 0);
 #pragma unroll
             for (int i = 0; i < 4; ++i) dst[4 * k + i] = (unsigned)v[i];
+        }
+    }
+}
+
+// One S24 chunk of CW elements (3 CW bytes at byte offset off of the slab; a = the slab base address
+// mod 4) -> CW fp32 words.  8 / 4 elements: 12-byte loads (4-aligned: level offsets and slot strides are
+// multiples of 4 bytes there).  2 elements (level 3, 6 bytes, 2-aligned): a naturally aligned word +
+// short pair chosen by the address parity — no load reaches outside the chunk, so the slab bound and
+// kOOB zeros stay exact.
+template <int CW>
+__device__ __forceinline__ void buf_s24(unsigned (&dst)[CW], __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned a) {
+    if constexpr ((RMD_LOOKUP_ABL & 2) != 0) off = kOOB;
+    if constexpr (CW == 2) {
+        const bool odd = ((off + a) & 2u) != 0;
+        const unsigned w = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(odd ? off + 2u : off), 0, 0);
+        const unsigned h = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(odd ? off : off + 4u), 0, 0);
+        // even: bytes 0-3 = w, 4-5 = h; odd: bytes 0-1 = h, 2-5 = w
+        dst[0] = odd ? (h << 8) | (w << 24) : w << 8;
+        dst[1] = odd ? w & 0xffffff00u : ((w >> 24) << 8) | (h << 16);
+    } else {
+#pragma unroll
+        for (int k = 0; k < CW / 4; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
+            const unsigned w0 = (unsigned)v[0], w1 = (unsigned)v[1], w2 = (unsigned)v[2];
+            dst[4 * k + 0] = w0 << 8;
+            dst[4 * k + 1] = __builtin_amdgcn_perm(w1, w0, 0x0504030Cu);
+            dst[4 * k + 2] = __builtin_amdgcn_perm(w2, w1, 0x0403020Cu);
+            dst[4 * k + 3] = w2 & 0xffffff00u;
         }
     }
 }
@@ -256,13 +298,16 @@ __device__ __forceinline__ bool level_setup(const PyrGeom& g, int L, float x, fl
 // BUF (per-image level slabs < 2^31 B): buffer loads, zeros for chunks off the level from kOOB, and
 // per-element padding masks only in waves where some lane's window reaches past the level's right
 // edge (MASK; a chunk there holds padding columns).  Rows off the level are whole chunks off the level.
+// S24 chunks are widened to fp32 words as they arrive and then shifted like an f32 level.
 template <typename T, int R, int L, int PR, bool MASK>
-__device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, const PyrGeom& g, int slot, int N,
+__device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, unsigned a, const PyrGeom& g, int slot, int N,
                                               float fx, float fy, int xs, int ys, const OutBuf& ob, int own0, int bb0) {
+    constexpr bool S24 = kIsS24<T>;
+    using TE = typename std::conditional<S24, float, T>::type;     // element type of the loaded words
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KR = PR + 1;
     constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 elements
     constexpr int CB = CW * (int)sizeof(T);                         // chunk bytes
-    constexpr int CWW = CB / 4;                                     // chunk words
+    constexpr int CWW = S24 ? CW : CB / 4;                          // chunk words (S24: widened)
     constexpr int NC = (K + CW - 1 + CW - 1) / CW;                  // chunks a row can span
     const int lh = g.lh[L], lw = g.lw[L], txs = g.tx[L];
     const unsigned cs = (unsigned)g.slots * CB, rsb = (unsigned)txs * cs;
@@ -282,13 +327,16 @@ __device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, const P
             const int tc = tc0 + c;
             const bool valid = rv && tc >= 0 && tc < txs && c * CW < sh + K;
             unsigned tmp[CWW];
-            buf_words<CWW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB);
+            if constexpr (S24)
+                buf_s24<CW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB, a);
+            else
+                buf_words<CWW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB);
 #pragma unroll
             for (int i = 0; i < CWW; ++i) wd[c * CWW + i] = tmp[i];
         }
         wd[NC * CWW] = 0u;
         float v[K];
-        shift_extract<T, K, CW, NC * CWW, MASK>(wd, sh, xs, lw, true, v);
+        shift_extract<TE, K, CW, NC * CWW, MASK>(wd, sh, xs, lw, true, v);
         float hcur[D];
 #pragma unroll
         for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
@@ -313,34 +361,37 @@ __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, con
     const int lh = g.lh[L], lw = g.lw[L];
     if constexpr (BUF) {
         const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
+        const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)level_base(pyr, g, L, b)) & 3u;
         if (__any(xs + K > lw))
-            rows_body_buf<T, R, L, PR, true>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+            rows_body_buf<T, R, L, PR, true>(rs, a, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
         else
-            rows_body_buf<T, R, L, PR, false>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+            rows_body_buf<T, R, L, PR, false>(rs, a, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
         return;
-    }
-    const T* lvl = pyr + g.off[L];
-    constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 (tiles layout: only L >= 2)
-    const long long chunk_stride = (long long)g.slots * CW;         // next chunk of the same row
-    const long long bq = (long long)b * g.ty[L];
-    const int txs = g.tx[L];
+    } else {
+        static_assert(!kIsS24<T>, "S24 pyramids are read through buffer loads only");
+        const T* lvl = pyr + g.off[L];
+        constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 (tiles layout: only L >= 2)
+        const long long chunk_stride = (long long)g.slots * CW;         // next chunk of the same row
+        const long long bq = (long long)b * g.ty[L];
+        const int txs = g.tx[L];
 
-    float hprev[D];
+        float hprev[D];
 #pragma unroll
-    for (int jj = 0; jj < KR; ++jj) {
-        const int j = bb0 + jj;
-        const int yy = ys + j;
-        const bool row_ok = yy >= 0 && yy < lh;
-        const int yc = min(max(yy, 0), lh - 1);
-        const T* row_ptr = lvl + ((bq + yc) * txs) * chunk_stride + (long long)slot * CW;
-        float v[K];
-        load_row<T, R, CW>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
-        float hcur[D];
+        for (int jj = 0; jj < KR; ++jj) {
+            const int j = bb0 + jj;
+            const int yy = ys + j;
+            const bool row_ok = yy >= 0 && yy < lh;
+            const int yc = min(max(yy, 0), lh - 1);
+            const T* row_ptr = lvl + ((bq + yc) * txs) * chunk_stride + (long long)slot * CW;
+            float v[K];
+            load_row<T, R, CW>(row_ptr, chunk_stride, txs, xs, lw, row_ok, v);
+            float hcur[D];
 #pragma unroll
-        for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
-        if (jj > 0 && active && (PR == D || j - 1 >= own0)) emit_row<D>(o, N, j - 1, fy, hprev, hcur);
+            for (int a = 0; a < D; ++a) hcur[a] = fmaf(fx, v[a + 1] - v[a], v[a]);
+            if (jj > 0 && active && (PR == D || j - 1 >= own0)) emit_row<D>(o, N, j - 1, fy, hprev, hcur);
 #pragma unroll
-        for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
+            for (int a = 0; a < D; ++a) hprev[a] = hcur[a];
+        }
     }
 }
 
@@ -566,10 +617,14 @@ int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coord
         buf = buf && (double)d.tiles_y[l] * d.tiles_x[l] * d.query_slots * d.tile_h[l] * d.tile_w[l] * sizeof(T) <
                          2147483648.0;
     buf = buf && (double)(2 * radius + 1) * (2 * radius + 1) * d.height * d.width * 4.0 < 2147483648.0;   // output block
+    if (kIsS24<T> && !buf) {
+        set_error("rmd_corr_lookup: S24 pyramids need per-image level slabs < 2 GiB");
+        return RMD_ERR_SHAPE;
+    }
     switch (radius) {
 #define RMD_CASE(RR) case RR: \
         if (buf) corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY, true><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
-        else corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY, false><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
+        else if constexpr (!kIsS24<T>) corr_lookup_kernel<T, RR, (2 * RR + 3) / 3, LAY, false><<<grid, kThreads, 0, st>>>(p, g, coords, zmask, out); \
         break;
         RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE
@@ -598,6 +653,8 @@ extern "C" int rmd_corr_lookup(const void* pyramid, const rmd_pyramid_desc* d, c
         return rmd::launch_lookup<__half, RMD_LAYOUT_ROWS>(pyramid, *d, coords, radius, zero_level_mask, out, st);
     if (d->storage == RMD_F32)
         return rmd::launch_lookup<float, RMD_LAYOUT_ROWS>(pyramid, *d, coords, radius, zero_level_mask, out, st);
-    rmd::set_error("rmd_corr_lookup: storage must be F32 or F16");
+    if (d->storage == RMD_S24)
+        return rmd::launch_lookup<rmd::s24_t, RMD_LAYOUT_ROWS>(pyramid, *d, coords, radius, zero_level_mask, out, st);
+    rmd::set_error("rmd_corr_lookup: storage must be F32, F16 or S24");
     return RMD_ERR_ARG;
 }

@@ -1135,7 +1135,11 @@ int check_args(const rmd_pyramid_desc* d, int channels, int compute) {
     RMD_REQUIRE(d->levels >= 1 && d->levels <= RMD_MAX_LEVELS, RMD_ERR_SHAPE, "rmd_corr_pyramid: bad levels");
     RMD_REQUIRE(compute == RMD_F32 || compute == RMD_BF16 || compute == RMD_BF16X3, RMD_ERR_ARG,
                 "rmd_corr_pyramid: compute must be F32, BF16 or BF16X3");
-    RMD_REQUIRE(d->storage == RMD_F32 || d->storage == RMD_F16, RMD_ERR_ARG, "rmd_corr_pyramid: storage must be F32 or F16");
+    RMD_REQUIRE(d->storage == RMD_F32 || d->storage == RMD_F16 || d->storage == RMD_S24, RMD_ERR_ARG,
+                "rmd_corr_pyramid: storage must be F32, F16 or S24");
+    RMD_REQUIRE(d->storage != RMD_S24 || gemm_path(*d, channels, compute) == Path::X3, RMD_ERR_ARG,
+                "rmd_corr_pyramid: S24 storage is written by the BF16X3 GEMM only (C <= 256; describe with "
+                "rmd_pyramid_describe_for)");
     const int want = path_layout(gemm_path(*d, channels, compute));
     RMD_REQUIRE(d->layout == want, RMD_ERR_ARG,
                 "rmd_corr_pyramid: the %s GEMM writes layout %d, desc has layout %d (describe with rmd_pyramid_describe_for)",
@@ -1150,6 +1154,9 @@ extern "C" int rmd_pyramid_describe_for(int batch, int height, int width, int le
                                         int compute, rmd_pyramid_desc* d) {
     int rc = rmd_pyramid_describe_layout(batch, height, width, levels, storage, RMD_LAYOUT_ROWS, d);
     if (rc || channels <= 0) return rc;
+    // S24 is an output format of the x3 GEMM: any other GEMM of this call stores F32
+    if (storage == RMD_S24 && rmd::gemm_path(*d, channels, compute) != rmd::Path::X3)
+        return rmd_pyramid_describe_layout(batch, height, width, levels, RMD_F32, RMD_LAYOUT_ROWS, d);
     if (rmd::gemm_path(*d, channels, compute) == rmd::Path::W8)
         rc = rmd_pyramid_describe_layout(batch, height, width, levels, storage, RMD_LAYOUT_TILES, d);
     return rc;

@@ -153,6 +153,7 @@ struct Lvl {
     unsigned cs;      // chunk stride (bytes)
     int rows;         // valid rows of this block on the level
     int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
+    unsigned a;       // base address mod 4 (S24 level 3 aligns its word store with it)
 };
 
 __device__ __forceinline__ unsigned soff(const Lvl& L, int row, int chunk) {
@@ -174,20 +175,22 @@ __device__ __forceinline__ void swapf(float& x, float& y) {
 
 constexpr int AUX_NT = 2;     // non-temporal stores: the pyramid is re-read a whole GEMM later
 
-// Epilogue of one 32-query tile: acc[ti] (ti = 2 rg + cg) holds, for lane (j, h), the targets
-// (row 4 rg + k, col 8 cg + 4 h + e) at acc[ti][4k + e].
-#ifndef RMD_X3_S24TEST
-#define RMD_X3_S24TEST 0
-#endif
 typedef __attribute__((ext_vector_type(3))) int i32x3;
-// 4 floats -> 3 words of their top 24 bits (rounded), for the 24-bit storage timing variant
+// RMD_S24 (include/rmd.h): a float rounded to its top 24 bits (round half away from zero on the
+// magnitude; a NaN stays a quiet NaN), kept in bytes 1..3 of the returned word
+__device__ __forceinline__ unsigned s24_round(float v) {
+    const unsigned u = __float_as_uint(v);
+    return (u & 0x7fffffffu) > 0x7f800000u ? (u | 0x00400000u) : u + 0x80u;
+}
+// 4 floats -> the 12 bytes of their S24 values (3 words)
 __device__ __forceinline__ i32x3 pack24(float a, float b, float c, float d) {
-    const unsigned v0 = __float_as_uint(a) + 0x80u, v1 = __float_as_uint(b) + 0x80u;
-    const unsigned v2 = __float_as_uint(c) + 0x80u, v3 = __float_as_uint(d) + 0x80u;
+    const unsigned v0 = s24_round(a), v1 = s24_round(b), v2 = s24_round(c), v3 = s24_round(d);
     return i32x3{(int)__builtin_amdgcn_perm(v1, v0, 0x05030201u), (int)__builtin_amdgcn_perm(v2, v1, 0x06050302u),
                  (int)__builtin_amdgcn_perm(v3, v2, 0x07060503u)};
 }
 
+// Epilogue of one 32-query tile (32x32x16 form, F32 storage): acc[ti] (ti = 2 rg + cg) holds, for
+// lane (j, h), the targets (row 4 rg + k, col 8 cg + 4 h + e) at acc[ti][4k + e].
 __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[4], int q, int h) {
     const unsigned qo[4] = {(unsigned)q * 32u + 16u * h, (unsigned)q * 32u + 16u * h, (unsigned)q * 16u + 8u * h,
                             (unsigned)q * 8u + 4u * h};
@@ -196,16 +199,10 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
     for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-#if RMD_X3_S24TEST
-            const i32x3 d3 = pack24(acc[ti][4 * k + 0], acc[ti][4 * k + 1], acc[ti][4 * k + 2], acc[ti][4 * k + 3]);
-            __builtin_amdgcn_raw_buffer_store_b96(d3, L[0].rsrc, (int)((qo[0] + soff(L[0], 4 * (ti >> 1) + k, ti & 1)) / 4u * 3u),
-                                                  0, AUX_NT);
-#else
             const i32x4 d = {__float_as_int(acc[ti][4 * k + 0]), __float_as_int(acc[ti][4 * k + 1]),
                              __float_as_int(acc[ti][4 * k + 2]), __float_as_int(acc[ti][4 * k + 3])};
             __builtin_amdgcn_raw_buffer_store_b128(d, L[0].rsrc, (int)(qo[0] + soff(L[0], 4 * (ti >> 1) + k, ti & 1)),
                                                    0, AUX_NT);
-#endif
         }
     // level 1: tile rows (2m, 2m+1) -> level-1 row 2rg + m; lane pair u -> block col 4cg + 2h + u
     float s2[2][2];      // level-2 sums [rg][cg] (16 level-0 values each)
@@ -231,14 +228,9 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[4], const Lvl (&L)[
             float x0 = p[0][0], x1 = p[0][1], y0 = p[1][0], y1 = p[1][1];
             swapf(x0, y0);
             swapf(x1, y1);
-#if RMD_X3_S24TEST
-            __builtin_amdgcn_raw_buffer_store_b96(pack24(0.25f * x0, 0.25f * x1, 0.25f * y0, 0.25f * y1), L[1].rsrc,
-                                                  (int)((qo[1] + soff(L[1], 2 * rg + m, 0)) / 4u * 3u), 0, AUX_NT);
-#else
             const i32x4 d = {__float_as_int(0.25f * x0), __float_as_int(0.25f * x1), __float_as_int(0.25f * y0),
                              __float_as_int(0.25f * y1)};
             __builtin_amdgcn_raw_buffer_store_b128(d, L[1].rsrc, (int)(qo[1] + soff(L[1], 2 * rg + m, 0)), 0, AUX_NT);
-#endif
         }
     }
     // level 2: row rg, lane holds col h (cg 0) and 2 + h (cg 1); after the swap lower = {0,1}, upper = {2,3}
@@ -566,17 +558,26 @@ __device__ __forceinline__ void ksteps16(f32x4 (&acc)[8][2], bf16x8 (&acur)[8], 
 
 // Epilogue of one 32-query tile in the 16x16 layout: acc[mt][u][e] is, for lane (n, g) and query
 // 16 u + n, the target (row 2 rp + (g >> 1), col 8 ch + 4 (g & 1) + e) with mt = 2 rp + ch.
+// S24: RMD_S24 storage (3 bytes per element; the Lvl strides are in those bytes): lanes gather whole
+// 12-byte pieces (4 values) before each store.
+template <bool S24>
 __device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (&L)[4], int qt, int N, int n, int g) {
+    constexpr unsigned E = S24 ? 3u : 4u;                  // bytes per element
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const unsigned q = (unsigned)min(qt * 32 + 16 * u + n, N - 1);
-        // level 0: 1 x 8 fp32 chunks (32 B per query); lanes g = 2 r', 2 r' + 1 write row r' bytes 0-15 / 16-31
+        // level 0: 1 x 8 chunks (8E bytes per query); lanes g = 2 r', 2 r' + 1 write row r' halves
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
-            const i32x4 d = {__float_as_int(acc[mt][u][0]), __float_as_int(acc[mt][u][1]), __float_as_int(acc[mt][u][2]),
-                             __float_as_int(acc[mt][u][3])};
-            __builtin_amdgcn_raw_buffer_store_b128(
-                d, L[0].rsrc, (int)(q * 32u + 16u * (g & 1) + soff(L[0], 2 * (mt >> 1) + (g >> 1), mt & 1)), 0, AUX_NT);
+            const unsigned o = q * 8u * E + 4u * E * (g & 1) + soff(L[0], 2 * (mt >> 1) + (g >> 1), mt & 1);
+            if constexpr (S24) {
+                __builtin_amdgcn_raw_buffer_store_b96(pack24(acc[mt][u][0], acc[mt][u][1], acc[mt][u][2], acc[mt][u][3]),
+                                                      L[0].rsrc, (int)o, 0, AUX_NT);
+            } else {
+                const i32x4 d = {__float_as_int(acc[mt][u][0]), __float_as_int(acc[mt][u][1]),
+                                 __float_as_int(acc[mt][u][2]), __float_as_int(acc[mt][u][3])};
+                __builtin_amdgcn_raw_buffer_store_b128(d, L[0].rsrc, (int)o, 0, AUX_NT);
+            }
         }
         // level 1: horizontal pairs in-lane, vertical pairs across the lane halves (ch 0 lands in the lower,
         // ch 1 in the upper half): lane g then holds level-1 cols 2g, 2g+1 of level-1 row rp
@@ -589,28 +590,64 @@ __device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (
             swapf(x0, y0);
             swapf(x1, y1);
             const float s0 = x0 + y0, s1 = x1 + y1;
-            const i32x2 d = {__float_as_int(0.25f * s0), __float_as_int(0.25f * s1)};
-            __builtin_amdgcn_raw_buffer_store_b64(d, L[1].rsrc, (int)(q * 32u + 8u * g + soff(L[1], rp, 0)), 0, AUX_NT);
+            if constexpr (S24) {
+                // even g takes its odd neighbour's two columns (lane + 16): cols 2g .. 2g + 3 in one piece
+                const float s2 = __shfl_xor(s0, 16), s3 = __shfl_xor(s1, 16);
+                __builtin_amdgcn_raw_buffer_store_b96(
+                    pack24(0.25f * s0, 0.25f * s1, 0.25f * s2, 0.25f * s3), L[1].rsrc,
+                    (int)((g & 1) ? kBig : q * 8u * E + 6u * (g >> 1) * 2u + soff(L[1], rp, 0)), 0, AUX_NT);
+            } else {
+                const i32x2 d = {__float_as_int(0.25f * s0), __float_as_int(0.25f * s1)};
+                __builtin_amdgcn_raw_buffer_store_b64(d, L[1].rsrc, (int)(q * 32u + 8u * g + soff(L[1], rp, 0)), 0,
+                                                      AUX_NT);
+            }
             const float t = s0 + s1;
             t2[rp >> 1] = (rp & 1) ? t2[rp >> 1] + t : t;
         }
         // level 2: lane g holds level-2 col g of rows 0 and 1
 #pragma unroll
-        for (int y2 = 0; y2 < 2; ++y2)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(0.0625f * t2[y2]), L[2].rsrc,
-                                                  (int)(q * 16u + 4u * g + soff(L[2], y2, 0)), 0, AUX_NT);
-        // level 3: col x3 = level-2 cols 2 x3, 2 x3 + 1 (lanes g, g ^ 1 = lane ^ 16); even g store
+        for (int y2 = 0; y2 < 2; ++y2) {
+            if constexpr (S24) {
+                // lane g = 0 collects cols 0..3 (lanes + 16, + 32, + 48) and writes the 12-byte chunk
+                const int l = threadIdx.x & 63;
+                const float v = 0.0625f * t2[y2];
+                const float v1 = __shfl(v, (l + 16) & 63), v2 = __shfl(v, (l + 32) & 63), v3 = __shfl(v, (l + 48) & 63);
+                __builtin_amdgcn_raw_buffer_store_b96(pack24(v, v1, v2, v3), L[2].rsrc,
+                                                      (int)(g ? kBig : q * 4u * E + soff(L[2], y2, 0)), 0, AUX_NT);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(0.0625f * t2[y2]), L[2].rsrc,
+                                                      (int)(q * 16u + 4u * g + soff(L[2], y2, 0)), 0, AUX_NT);
+            }
+        }
+        // level 3: col x3 = level-2 cols 2 x3, 2 x3 + 1 (lanes g, g ^ 1 = lane ^ 16); even g hold col g >> 1
         float t3 = t2[0] + t2[1];
         t3 += __shfl_xor(t3, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int((1.0f / 64.0f) * t3), L[3].rsrc,
-                                              (int)((g & 1) ? kBig : q * 8u + 4u * (g >> 1) + soff(L[3], 0, 0)), 0, AUX_NT);
+        const float v3 = (1.0f / 64.0f) * t3;
+        if constexpr (S24) {
+            // lane g = 0 takes col 1 from lane + 32 and writes the 6-byte chunk as an aligned word + short
+            const float w1 = __shfl_xor(v3, 32);
+            const unsigned r0 = s24_round(v3), r1 = s24_round(w1);
+            const unsigned base = q * 2u * E + soff(L[3], 0, 0);       // 2-aligned (chunks are 6 bytes)
+            const bool odd = ((base + L[3].a) & 2u) != 0;
+            // even: word = bytes 0-3, short = bytes 4-5; odd: short = bytes 0-1, word = bytes 2-5
+            const unsigned word = odd ? __builtin_amdgcn_perm(r1, r0, 0x07060503u) : __builtin_amdgcn_perm(r1, r0, 0x05030201u);
+            const unsigned shrt = odd ? ((r0 >> 8) & 0xffffu) : (r1 >> 16);
+            __builtin_amdgcn_raw_buffer_store_b32((int)word, L[3].rsrc, (int)(g ? kBig : base + (odd ? 2u : 0u)), 0, AUX_NT);
+            __builtin_amdgcn_raw_buffer_store_b16((short)shrt, L[3].rsrc, (int)(g ? kBig : base + (odd ? 0u : 4u)), 0,
+                                                  AUX_NT);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v3), L[3].rsrc,
+                                                  (int)((g & 1) ? kBig : q * 8u + 4u * (g >> 1) + soff(L[3], 0, 0)), 0,
+                                                  AUX_NT);
+        }
     }
 }
 
-template <int ABL = 0>
+template <int ABL = 0, bool S24 = false>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
-                 const __bf16* __restrict__ bLo, PyrGeom g, int units, float* __restrict__ pyr) {
+                 const __bf16* __restrict__ bLo, PyrGeom g, int units, unsigned char* __restrict__ pyr) {
+    constexpr unsigned E = S24 ? 3u : 4u;                  // bytes per stored element
     constexpr int WAVES = 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = g.height, W = g.width, N = H * W;
@@ -663,18 +700,19 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
         const bool lv = l < g.levels;
         const int cw = g.tw[l];
         const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
-        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * 4u : 0u;
+        const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * E : 0u;
         const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-        float* bp = pyr + base;
+        unsigned char* bp = pyr + base * E;
         const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
         const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
         L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,
                                                       (int)__builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs),
                                                       0x00020000);
         L[l].rs = __builtin_amdgcn_readfirstlane(rs);
-        L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * 4u);
+        L[l].cs = __builtin_amdgcn_readfirstlane((unsigned)N * cw * E);
         L[l].rows = __builtin_amdgcn_readfirstlane(rows);
         L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
+        L[l].a = lo32 & 3u;
     }
 
     unsigned bhi = (unsigned)(gq * 128 + n) * 16u, blo = bhi + 65536u;
@@ -694,7 +732,7 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
                 rl[s][uu] = *reinterpret_cast<const bf16x8*>(p + uu * 4096 + 512 * s + lo_off);
             }
     }
-    vmcnt_pad_n<kEpiStores16>(pyr);
+    vmcnt_pad_n<S24 ? kEpiStores16 + 1 : kEpiStores16>(pyr);
     // ping-pong phases as corr_pyramid_x3: waves w and w + 4 of each SIMD alternate MFMA and epilogue
     const int nmax = (nqt + WAVES - 1) / WAVES;
     const int nw = qt < nqt ? (nqt - qt + WAVES - 1) / WAVES : 0;
@@ -709,7 +747,7 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
             ksteps16<0>(acc, a0, a1, rh, rl, smem, bhi, blo, bq + (size_t)qt * 8192, bq + (size_t)min(qn, nqt - 1) * 8192,
                         lo_off);
             __builtin_amdgcn_s_barrier();
-            epilogue16(acc, L, qt, N, n, gq);
+            epilogue16<S24>(acc, L, qt, N, n, gq);
             __builtin_amdgcn_s_barrier();
         } else {
             __builtin_amdgcn_s_barrier();
@@ -723,12 +761,20 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
 }  // namespace
 
 bool eligible(const rmd_pyramid_desc& d, int C) {
-    if (C > 256 || d.storage != RMD_F32 || d.levels < 1) return false;
+    if (C > 256 || (d.storage != RMD_F32 && d.storage != RMD_S24) || d.levels < 1 || d.layout != RMD_LAYOUT_ROWS)
+        return false;
     // every block's per-level store range (rows x row stride, bytes) plus the 1 GiB chunk bias must
     // stay inside 32-bit buffer offsets
     const double N = (double)d.height * d.width;
     const double span0 = 8.0 * d.tiles_x[0] * N * 8 * 4;
-    return span0 < (double)(1u << 30);
+    if (span0 >= (double)(1u << 30)) return false;
+    if (d.storage == RMD_S24) {
+        // the lookup reads S24 through per-image level buffers only: every slab below 2^31 bytes
+        for (int l = 0; l < d.levels; ++l)
+            if ((double)d.tiles_y[l] * d.tiles_x[l] * d.query_slots * d.tile_h[l] * d.tile_w[l] * 3.0 >= 2147483648.0)
+                return false;
+    }
+    return true;
 }
 
 size_t workspace_bytes(const rmd_pyramid_desc& d) {
@@ -760,12 +806,13 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
 #if RMD_X3_SHAPE == 16
     {
         const int units = nblk * d.batch;
-        auto kern = corr_pyramid_x3s<RMD_X3_ABL>;
+        auto kern = d.storage == RMD_S24 ? corr_pyramid_x3s<RMD_X3_ABL, true> : corr_pyramid_x3s<RMD_X3_ABL, false>;
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds16);
-        kern<<<units, 512, kLds16, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<float*>(pyr));
+        kern<<<units, 512, kLds16, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<unsigned char*>(pyr));
         return check_launch("rmd_corr_pyramid/gemm-x3");
     }
 #endif
+    if (d.storage != RMD_F32) return RMD_ERR_ARG;       // the 32x32x16 form stores F32 only
     // schedule (32x32x16 form, -DRMD_X3_SHAPE=32) (see corr_pyramid_x3): quarters Q in {1, 2, 4, 8} minimising slots x rounds per unit,
     // slots = ceil(B nblk Q / CUs) (one 137-KB-LDS workgroup per CU), rounds = ceil(nqt / Q / 8); a
     // unit re-stages A, charged as 0.3 round.  Q = 1 with one workgroup per unit is the plain launch

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (load torch's libamdhip64 first so librmd.so binds to the same HIP runtime)
 
 RMD_OK = 0
-RMD_F32, RMD_F16, RMD_BF16, RMD_BF16X3 = 0, 1, 2, 3
+RMD_F32, RMD_F16, RMD_BF16, RMD_BF16X3, RMD_S24 = 0, 1, 2, 3, 4
 RMD_LAYOUT_ROWS, RMD_LAYOUT_TILES = 0, 1
 MAX_LEVELS = 4
 

@@ -7,7 +7,8 @@ The correlation blocks it then constructs take only ``(fmap1, fmap2, num_levels,
 (raft.py:384, raft_fs.py:132).  The drop-in reads three more keys from that same ``parameters``
 section; all are optional and their defaults reproduce the reference:
 
-  corr-precision      fp32 (default: split-bf16 MFMA, fp32 pyramid, ~1e-5 of the reference) |
+  corr-precision      fp32 (default: split-bf16 MFMA, 24-bit pyramid (fp32 rounded to 16 significant
+                      bits), ~1e-5 of the reference) | fp32-f32 (same GEMM, fp32 pyramid) |
                       fp32-exact | bf16 (bf16 MFMA, fp16 pyramid: the bench mode) | bf16-f32 | fp32-f16
   corr-method         auto (default) | volume | otf — all-pairs pyramid + lookup, or the on-the-fly
                       lookup with no O(N^2) buffer (both differentiable); auto takes the volume unless
@@ -25,12 +26,12 @@ values.
 import re
 from collections import namedtuple
 
-PRECISIONS = ("fp32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16")
+PRECISIONS = ("fp32", "fp32-f32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16")
 METHODS = ("auto", "volume", "otf")
 KEYS = ("corr-precision", "corr-method", "corr-memory-budget")
 DEFAULTS = {"corr-precision": "fp32", "corr-method": "auto", "corr-memory-budget": 16 << 30}
 
-_STORAGE_BYTES = {"fp32": 4, "fp32-exact": 4, "bf16": 2, "bf16-f32": 4, "fp32-f16": 2}
+_STORAGE_BYTES = {"fp32": 3, "fp32-f32": 4, "fp32-exact": 4, "bf16": 2, "bf16-f32": 4, "fp32-f16": 2}
 
 
 class CorrOptions(namedtuple("CorrOptions", ["precision", "method", "memory_budget"])):

@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .library import LIB, _SCHEMAS, _STORAGE, _STORAGE_CODE, pyramid_layout
+from .library import LIB, _SCHEMAS, _STORAGE, pyramid_elements, pyramid_layout, pyramid_storage, s24_decode
 
 
 def _delta(r, device):
@@ -85,6 +85,10 @@ def _unpack(pyramid, desc, i):
 def corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
     f1, f2 = fmap1.float(), fmap2.float()
     b, c, h, w = f1.shape
+    if storage == _lib.RMD_S24:
+        # S24 is the x3 GEMM's output format; every other GEMM (this one too) stores F32, as
+        # rmd_pyramid_describe_for resolves it — which also keeps the ATen graph differentiable
+        storage = _lib.RMD_F32
     desc = _lib.describe(b, h, w, levels, storage, _lib.RMD_LAYOUT_ROWS)
     return _pack_rows(_corr_levels(f1, f2, levels, float(scale)), desc, _STORAGE[storage])
 
@@ -92,9 +96,12 @@ def corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
 def corr_lookup(pyramid, coords, levels, radius, level_mask):
     """raft.py:49-95 over the levels stored in `pyramid`."""
     b, _, h, w = coords.shape
-    desc = _lib.describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype], pyramid_layout(pyramid))
-    if pyramid.numel() != desc.total_elements:
-        raise ValueError(f"corr_lookup: coords {tuple(coords.shape)} do not match the pyramid ({pyramid.numel()} elements)")
+    desc = _lib.describe(b, h, w, levels, pyramid_storage(pyramid), pyramid_layout(pyramid))
+    if pyramid_elements(pyramid) != desc.total_elements:
+        raise ValueError(f"corr_lookup: coords {tuple(coords.shape)} do not match the pyramid "
+                         f"({pyramid_elements(pyramid)} elements)")
+    if desc.storage == _lib.RMD_S24:
+        pyramid = s24_decode(pyramid)
     r = radius
     co = coords.float().permute(0, 2, 3, 1)
     delta = _delta(r, coords.device)

@@ -130,13 +130,15 @@ def describe_for(batch, height, width, levels, storage, channels, compute):
     return d
 
 
-_STORAGE = {_lib.RMD_F32: torch.float32, _lib.RMD_F16: torch.float16}
-_STORAGE_CODE = {torch.float32: _lib.RMD_F32, torch.float16: _lib.RMD_F16}
+_STORAGE = {_lib.RMD_F32: torch.float32, _lib.RMD_F16: torch.float16, _lib.RMD_S24: torch.uint8}
+_STORAGE_CODE = {torch.float32: _lib.RMD_F32, torch.float16: _lib.RMD_F16, torch.uint8: _lib.RMD_S24}
 
-# The pyramid tensor carries its layout in its shape, so corr_lookup never trusts a caller's word for
-# it: RMD_LAYOUT_ROWS pyramids are 1-D (total_elements,), RMD_LAYOUT_TILES pyramids 2-D
-# (total_elements / 8, 8) — one row per 2 x 4 chunk (every tiles level holds a multiple of 64 elements).
+# The pyramid tensor carries its layout and storage in its shape and dtype, so corr_lookup never
+# trusts a caller's word for them: RMD_LAYOUT_ROWS pyramids are 1-D (total_elements,) float32/float16,
+# RMD_LAYOUT_TILES pyramids 2-D (total_elements / 8, 8) float16 — one row per 2 x 4 chunk (every tiles
+# level holds a multiple of 64 elements) — and RMD_S24 pyramids (row layout) uint8 (total_elements, 3).
 TILES_ROW = 8
+S24_BYTES = 3
 
 
 def pyramid_view(data, layout):
@@ -146,12 +148,50 @@ def pyramid_view(data, layout):
 
 def pyramid_layout(pyramid):
     """Layout of a pyramid tensor from its shape; ValueError for any other shape."""
-    if pyramid.dim() == 1:
+    if pyramid.dtype == torch.uint8:
+        if pyramid.dim() == 2 and pyramid.shape[1] == S24_BYTES:
+            return _lib.RMD_LAYOUT_ROWS
+    elif pyramid.dim() == 1:
         return _lib.RMD_LAYOUT_ROWS
-    if pyramid.dim() == 2 and pyramid.shape[1] == TILES_ROW:
+    elif pyramid.dim() == 2 and pyramid.shape[1] == TILES_ROW:
         return _lib.RMD_LAYOUT_TILES
-    raise ValueError(f"corr_lookup: a pyramid is 1-D (row layout) or (n, {TILES_ROW}) (tiles layout), "
-                     f"got shape {tuple(pyramid.shape)}")
+    raise ValueError(f"corr_lookup: a pyramid is 1-D (row layout), (n, {TILES_ROW}) (tiles layout) or uint8 "
+                     f"(n, {S24_BYTES}) (S24 storage), got {pyramid.dtype} {tuple(pyramid.shape)}")
+
+
+def pyramid_storage(pyramid):
+    """RMD_F32 / RMD_F16 / RMD_S24 of a pyramid tensor (its dtype)."""
+    if pyramid.dtype not in _STORAGE_CODE:
+        raise ValueError(f"corr_lookup: pyramid dtype must be float32, float16 or uint8 (S24), got {pyramid.dtype}")
+    return _STORAGE_CODE[pyramid.dtype]
+
+
+def pyramid_elements(pyramid):
+    """Pyramid elements held by a pyramid tensor (S24: 3 bytes each)."""
+    return pyramid.shape[0] if pyramid.dtype == torch.uint8 else pyramid.numel()
+
+
+def new_pyramid(like, d):
+    """Uninitialised pyramid tensor for desc d on like's device (like.new_empty: fake tensors too)."""
+    if d.storage == _lib.RMD_S24:
+        return like.new_empty((d.total_elements, S24_BYTES), dtype=torch.uint8)
+    return pyramid_view(like.new_empty((d.total_elements,), dtype=_STORAGE[d.storage]), d.layout)
+
+
+def s24_encode(x):
+    """float tensor -> RMD_S24 bytes (n, 3): the top 24 bits of each fp32 word, rounded half away from
+    zero on the magnitude; NaN stays a quiet NaN (include/rmd.h RMD_S24, the x3 GEMM's epilogue)."""
+    u = x.detach().float().contiguous().reshape(-1).view(torch.int32)
+    nan = (u & 0x7fffffff) > 0x7f800000
+    r = torch.where(nan, u | 0x00400000, u + 0x80)
+    return r.view(torch.uint8).view(-1, 4)[:, 1:4].contiguous()
+
+
+def s24_decode(b):
+    """RMD_S24 bytes (n, 3) -> float32 (n,) (low mantissa byte zero)."""
+    w = torch.zeros((b.shape[0], 4), dtype=torch.uint8, device=b.device)
+    w[:, 1:4] = b
+    return w.view(torch.float32).reshape(-1)
 
 
 # ---- RAFT correlation pyramid + lookup (inference operators) -----------------------------------
@@ -170,22 +210,22 @@ def _corr_pyramid(fmap1, fmap2, levels, compute, storage, scale):
     lib = _lib.lib()
     ws = torch.empty(lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), c, compute), dtype=torch.uint8,
                      device=f1.device)
-    data = torch.empty(d.total_elements, dtype=_STORAGE[storage], device=f1.device)
+    data = new_pyramid(f1, d)                         # d.storage: S24 falls back to F32 off the x3 GEMM
     with _Dev(f1) as st:
         _lib.check(lib.rmd_corr_pyramid(_ptr(f1), _ptr(f2), c, float(scale), ctypes.byref(d), compute, _ptr(data),
                                         _ptr(ws), st), "rmd_corr_pyramid")
-    return pyramid_view(data, d.layout)
+    return data
 
 
 @_fake("corr_pyramid")
 def _(fmap1, fmap2, levels, compute, storage, scale):
     _check_fmaps(fmap1, fmap2)
     b, c, h, w = fmap1.shape
-    if fmap1.device.type == "cpu":                  # rmd/cpu.py writes the row layout
-        d = describe(b, h, w, levels, storage)
+    if fmap1.device.type == "cpu":                  # rmd/cpu.py writes the row layout, S24 as F32
+        d = describe(b, h, w, levels, _lib.RMD_F32 if storage == _lib.RMD_S24 else storage)
     else:
         d = describe_for(b, h, w, levels, storage, c, compute)
-    return pyramid_view(fmap1.new_empty((d.total_elements,), dtype=_STORAGE[storage]), d.layout)
+    return new_pyramid(fmap1, d)
 
 
 def _lookup_out(pyramid, coords, levels, radius):
@@ -204,12 +244,12 @@ def _check_device(name, *ts):
 def _corr_lookup(pyramid, coords, levels, radius, level_mask):
     b, two, h, w = coords.shape
     if pyramid.dtype not in _STORAGE_CODE or not pyramid.is_contiguous():
-        raise ValueError(f"corr_lookup: pyramid must be a contiguous float32/float16 tensor, got "
+        raise ValueError(f"corr_lookup: pyramid must be a contiguous float32/float16/uint8 (S24) tensor, got "
                          f"{pyramid.dtype} {tuple(pyramid.shape)}")
     layout = pyramid_layout(pyramid)
     _check_device("corr_lookup", pyramid, coords)
-    d = describe(b, h, w, levels, _STORAGE_CODE[pyramid.dtype], layout)
-    if two != 2 or pyramid.numel() != d.total_elements:
+    d = describe(b, h, w, levels, pyramid_storage(pyramid), layout)
+    if two != 2 or pyramid_elements(pyramid) != d.total_elements:
         raise ValueError(f"corr_lookup: coords {tuple(coords.shape)} do not match the pyramid ({pyramid.numel()} elements)")
     co = _f32(coords)
     out = _lookup_out(pyramid, co, levels, radius)

@@ -12,11 +12,12 @@ import ctypes
 import torch
 
 from . import _lib, config, library
-from ._lib import RMD_BF16, RMD_BF16X3, RMD_F16, RMD_F32
+from ._lib import RMD_BF16, RMD_BF16X3, RMD_F16, RMD_F32, RMD_S24
 
 # precision modes: (GEMM compute type, pyramid storage type)
 PRECISIONS = {
-    "fp32": (RMD_BF16X3, RMD_F32),    # fp32-accurate split-bf16 MFMA (3 products), f32 pyramid: parity mode (default)
+    "fp32": (RMD_BF16X3, RMD_S24),    # fp32-accurate split-bf16 MFMA (3 products), 24-bit pyramid: parity mode (default)
+    "fp32-f32": (RMD_BF16X3, RMD_F32),# the same GEMM, f32 pyramid
     "fp32-exact": (RMD_F32, RMD_F32), # exact f32 MFMA (v_mfma_f32_32x32x2_f32), f32 pyramid
     "bf16": (RMD_BF16, RMD_F16),      # bf16 MFMA operands, f32 accumulate, fp16 pyramid: perf mode
     "bf16-f32": (RMD_BF16, RMD_F32),  # bf16 operands, f32 pyramid
@@ -57,12 +58,9 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-_STORAGE_DTYPE = {RMD_F32: torch.float32, RMD_F16: torch.float16}
-
-
 class Pyramid:
     """Correlation pyramid in the tiled, query-minor HBM layout of include/rmd.h.  ``data`` is 1-D in the
-    row layout and (n, 8) in the tiles layout (rmd.library.pyramid_view)."""
+    row layout, (n, 8) in the tiles layout (rmd.library.pyramid_view) and uint8 (n, 3) with RMD_S24 storage."""
 
     def __init__(self, data, desc, channels, scale):
         self.data = data
@@ -85,7 +83,8 @@ class Pyramid:
         hl, wl = d.level_h[i], d.level_w[i]
         s = d.query_slots
         off = d.level_offset[i]
-        x = self.data.reshape(-1)[off: off + b * ty * tx * s * th * tw].view(b, ty, tx, s, th, tw)
+        flat = library.s24_decode(self.data) if d.storage == RMD_S24 else self.data.reshape(-1)
+        x = flat[off: off + b * ty * tx * s * th * tw].view(b, ty, tx, s, th, tw)
         x = x.permute(0, 3, 1, 4, 2, 5).reshape(b, s, ty * th, tx * tw)[..., :hl, :wl]
         if d.layout == _lib.RMD_LAYOUT_TILES:
             x = x.index_select(1, torch.as_tensor(tiles_slots(h, w), device=x.device))
@@ -118,7 +117,9 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     scale = 1.0 / float(c) ** 0.5 if scale is None else float(scale)
     if events is None:
         data = torch.ops.rmd.corr_pyramid(fmap1, fmap2, levels, compute, storage, scale)
-        return Pyramid(data, library.describe(b, h, w, levels, storage, library.pyramid_layout(data)), c, scale)
+        # the storage the GEMM wrote (S24 is the x3 GEMM's alone: other GEMMs of the call store F32)
+        d = library.describe(b, h, w, levels, library.pyramid_storage(data), library.pyramid_layout(data))
+        return Pyramid(data, d, c, scale)
     _require_gpu(fmap1, fmap2)
     d = library.describe_for(b, h, w, levels, storage, c, compute)
     f1 = fmap1.detach().float().contiguous()
@@ -126,8 +127,7 @@ def corr_pyramid(fmap1, fmap2, levels=4, precision=None, events=None, scale=None
     lib = _lib.lib()
     ws = torch.empty(lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), c, compute), dtype=torch.uint8,
                      device=f1.device)
-    data = library.pyramid_view(torch.empty(d.total_elements, dtype=_STORAGE_DTYPE[storage], device=f1.device),
-                                d.layout)
+    data = library.new_pyramid(f1, d)
     with torch.cuda.device(f1.device):
         stream = _lib.stream_ptr(f1.device)
         _lib.check(lib.rmd_corr_prepare(_ptr(f1), _ptr(f2), c, scale, ctypes.byref(d), compute, _ptr(ws), stream),

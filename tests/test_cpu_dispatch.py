@@ -24,7 +24,9 @@ def _t(a, grad=False):
     return torch.from_numpy(np.ascontiguousarray(a)).requires_grad_(grad)
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 0.0), ("fp32-exact", 0.0), ("bf16", 1e-2)])
+# the CPU GEMM stores F32 for fp32 (S24 is the x3 GEMM's format): the fp32 modes reproduce the
+# reference bit for bit
+@pytest.mark.parametrize("precision,tol", [("fp32", 0.0), ("fp32-f32", 0.0), ("fp32-exact", 0.0), ("bf16", 1e-2)])
 @pytest.mark.parametrize("name", CORR_CASES)
 def test_corr_block_cpu_matches_reference_golden(name, precision, tol):
     import rmd
@@ -35,15 +37,55 @@ def test_corr_block_cpu_matches_reference_golden(name, precision, tol):
     assert out.device.type == "cpu" and out.dtype == torch.float32 and out.is_contiguous()
     assert tuple(out.shape) == g["out"].shape
     assert rel_max_err(out.numpy(), g["out"]) <= tol
-    assert cb.pyramid.data.dim() == 1                 # CPU pyramids are in the row layout
+    assert rmd.library.pyramid_layout(cb.pyramid.data) == rmd._lib.RMD_LAYOUT_ROWS   # CPU pyramids: row layout
 
 
-def test_corr_pyramid_levels_cpu():
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-6), ("fp32-f32", 1e-6)])
+def test_corr_pyramid_levels_cpu(precision, tol):
     import rmd
     g = load_golden("corr_b1_c256_16x24_pyr")
-    cb = rmd.raft.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), 4, 4, precision="fp32")
+    cb = rmd.raft.CorrBlock(_t(g["fmap1"]), _t(g["fmap2"]), 4, 4, precision=precision)
     for i, lvl in enumerate(cb.corr_pyramid):
-        assert rel_max_err(lvl.numpy(), g[f"pyr{i}"]) < 1e-6
+        assert rel_max_err(lvl.numpy(), g[f"pyr{i}"]) < tol
+
+
+def test_s24_encoding_rounds_half_away_and_keeps_specials():
+    """RMD_S24 (include/rmd.h): top 24 bits of the fp32 word, round half away from zero on the
+    magnitude; inf stays inf, NaN stays NaN, the largest finite values round to inf."""
+    import rmd
+    lib = rmd.library
+    x = torch.tensor([0.0, -0.0, 1.0, -1.0, 1.0 + 2.0 ** -17, 1.0 + 2.0 ** -16, 1.0 + 3 * 2.0 ** -17,
+                      float("inf"), float("-inf"), float("nan"), 3.4028235e38, -3.4028235e38, 1e-40],
+                     dtype=torch.float32)
+    y = lib.s24_decode(lib.s24_encode(x))
+    # 15 stored mantissa bits: ulp(1) = 2^-15, ties (1 + 2^-16) round away from zero
+    exp = torch.tensor([0.0, -0.0, 1.0, -1.0, 1.0, 1.0 + 2.0 ** -15, 1.0 + 2.0 ** -15,
+                        float("inf"), float("-inf"), float("nan"), float("inf"), float("-inf"), 0.0])
+    exp[-1] = lib.s24_decode(lib.s24_encode(torch.tensor([1e-40])))[0]    # subnormal: 8 low bits dropped
+    assert torch.equal(torch.signbit(y), torch.signbit(exp))
+    assert torch.equal(torch.isnan(y), torch.isnan(exp))
+    m = ~torch.isnan(exp)
+    assert torch.equal(y[m], exp[m])
+    r = torch.randn(100000) * torch.exp(torch.randn(100000) * 10)
+    assert ((lib.s24_decode(lib.s24_encode(r)) - r).abs() <= r.abs() * 2.0 ** -16).all()
+
+
+def test_cpu_lookup_reads_s24_pyramids():
+    """An S24 pyramid (uint8 (n, 3), the x3 GEMM's output) looked up on the CPU equals the lookup of
+    its decoded f32 values; its shape and dtype carry the storage."""
+    import rmd
+    g = load_golden("corr_b2_c32_24x40")
+    f1, f2, co = _t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"])
+    lv, r = int(g["levels"]), int(g["radius"])
+    p32 = torch.ops.rmd.corr_pyramid(f1, f2, lv, rmd._lib.RMD_BF16X3, rmd._lib.RMD_S24, 1.0 / 32 ** 0.5)
+    assert p32.dtype == torch.float32 and p32.dim() == 1          # the CPU GEMM stores F32
+    p24 = rmd.library.s24_encode(p32)
+    assert p24.dtype == torch.uint8 and p24.shape == (p32.numel(), 3)
+    assert rmd.library.pyramid_storage(p24) == rmd._lib.RMD_S24
+    a = torch.ops.rmd.corr_lookup(p24, co, lv, r, 0)
+    b = torch.ops.rmd.corr_lookup(rmd.library.s24_decode(p24), co, lv, r, 0)
+    assert torch.equal(a, b)
+    assert rel_max_err(a.numpy(), g["out"]) < 2e-5
 
 
 @pytest.mark.parametrize("name", ["corr_fs_b2_c32_24x40", "corr_fs_b2_c16_16x24_nonfinite"])

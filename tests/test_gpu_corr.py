@@ -19,7 +19,7 @@ from conftest import assert_close_elementwise, load_golden, rel_max_err
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": 1e-4, "fp32-exact": 1e-4, "bf16": 1e-2, "bf16-f32": 1e-2, "fp32-f16": 2e-3}
+TOL = {"fp32": 1e-4, "fp32-f32": 1e-4, "fp32-exact": 1e-4, "bf16": 1e-2, "bf16-f32": 1e-2, "fp32-f16": 2e-3}
 CORR_CASES = ["corr_b2_c32_24x40", "corr_b2_c32_24x40_mask", "corr_b1_c256_16x24_pyr",
               "corr_b1_c16_12x20_nan", "corr_b1_c32_20x28_r7_l2", "corr_b2_c64_17x23_l1",
               "corr_b2_c16_16x24_nonfinite"]      # NaN / +-inf coordinates -> NaN windows (grid_sample)
@@ -30,7 +30,7 @@ def _t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-f32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16"])
 @pytest.mark.parametrize("name", CORR_CASES)
 def test_corr_block_matches_reference_golden(name, precision):
     import rmd
@@ -44,7 +44,7 @@ def test_corr_block_matches_reference_golden(name, precision):
     assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32-exact", 1e-5), ("fp32", 1e-4)])
+@pytest.mark.parametrize("precision,tol", [("fp32-exact", 1e-5), ("fp32", 1e-4), ("fp32-f32", 1e-4)])
 def test_pyramid_levels_match_reference_golden(precision, tol):
     import rmd
     g = load_golden("corr_b1_c256_16x24_pyr")
@@ -469,3 +469,53 @@ def test_pyramid_tensor_carries_its_layout_48x64():
     assert rel_max_err(out, ref) < TOL["bf16"]
     with pytest.raises(ValueError, match="tiles layout"):
         torch.ops.rmd.corr_lookup(pyr.view(-1, 16), _t(co), 4, 4, 0)
+
+
+@pytest.mark.parametrize("c,b,h,w", [(256, 8, 55, 128), (96, 3, 9, 70), (200, 2, 23, 40), (256, 1, 8, 8),
+                                     (64, 1, 17, 33), (256, 2, 46, 62)])
+def test_s24_pyramid_is_rounded_f32_pyramid(c, b, h, w):
+    """The x3 GEMM's S24 epilogue (fp32 mode) against its F32 epilogue (fp32-f32) on the same inputs:
+    every stored element equals the F32 value rounded by the RMD_S24 rule (rmd.library.s24_encode),
+    bit for bit — all four levels, odd / even query parity of the 6-byte level-3 chunks, ragged maps and
+    C < 256 — and the lookup of the S24 pyramid equals the lookup of its decoded f32 values."""
+    import rmd
+    from rmd import _lib, library
+    rng = np.random.default_rng(c * 7 + h * w + b)
+    f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
+    f1[0, :, 0, 0] = np.nan                                         # a NaN query row stays NaN
+    p24 = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "fp32")
+    p32 = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "fp32-f32")
+    assert p24.desc.storage == _lib.RMD_S24 and p24.data.dtype == torch.uint8
+    assert p24.data.shape == (p32.desc.total_elements, 3)
+    enc = library.s24_encode(p32.data)
+    assert torch.equal(p24.data, enc)
+    ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    co = _t((np.stack([xs, ys])[None] + rng.normal(0, 3, (b, 2, h, w))).astype(np.float32))
+    a = torch.ops.rmd.corr_lookup(p24.data, co, 4, 4, 0)
+    r = torch.ops.rmd.corr_lookup(library.s24_decode(p24.data), co, 4, 4, 0)
+    assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(r, nan=7.0))
+
+
+def test_s24_storage_falls_back_to_f32_off_the_x3_gemm():
+    """S24 is the x3 GEMM's output format: describe_for resolves it to F32 for any other GEMM (C > 256,
+    exact f32, bf16) and rmd_corr_pyramid refuses an S24 desc there."""
+    import rmd
+    from rmd import _lib
+    d = _lib.describe_for(1, 16, 24, 4, _lib.RMD_S24, 320, _lib.RMD_BF16X3)        # C > 256: tiled f32
+    assert d.storage == _lib.RMD_F32
+    d = _lib.describe_for(1, 16, 24, 4, _lib.RMD_S24, 256, _lib.RMD_BF16X3)
+    assert d.storage == _lib.RMD_S24
+    f = torch.randn(1, 320, 16, 24, device=DEV)
+    pyr = torch.ops.rmd.corr_pyramid(f, f, 4, _lib.RMD_BF16X3, _lib.RMD_S24, 1.0)
+    assert pyr.dtype == torch.float32 and pyr.dim() == 1
+    with pytest.raises(RuntimeError, match="S24"):
+        d = _lib.describe(1, 16, 24, 4, _lib.RMD_S24)
+        lib = _lib.lib()
+        import ctypes
+        ws = torch.empty(lib.rmd_corr_pyramid_workspace_bytes(ctypes.byref(d), 320, _lib.RMD_F32), dtype=torch.uint8,
+                         device=DEV)
+        out = torch.empty(d.total_elements * 3, dtype=torch.uint8, device=DEV)
+        _lib.check(lib.rmd_corr_pyramid(ctypes.c_void_p(f.data_ptr()), ctypes.c_void_p(f.data_ptr()), 320, 1.0,
+                                        ctypes.byref(d), _lib.RMD_F32, ctypes.c_void_p(out.data_ptr()),
+                                        ctypes.c_void_p(ws.data_ptr()), None), "rmd_corr_pyramid")

@@ -37,6 +37,11 @@ def test_fake_kernels_propagate_shapes():
         rows = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16X3, _lib.RMD_F32, 0.0625)
         assert rows.dim() == 1                                                       # row layout: 1-D
         assert torch.ops.rmd.corr_lookup(rows, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        s24 = torch.ops.rmd.corr_pyramid(f1, f1, 4, _lib.RMD_BF16X3, _lib.RMD_S24, 0.0625)
+        assert s24.dtype == torch.uint8 and s24.shape == (rows.numel(), 3)          # S24: (n, 3) bytes
+        assert torch.ops.rmd.corr_lookup(s24, co, 4, 4, 0).shape == (2, 324, 55, 128)
+        f320 = torch.empty(2, 320, 55, 128, device="cuda")                           # C > 256: no x3 -> F32
+        assert torch.ops.rmd.corr_pyramid(f320, f320, 4, _lib.RMD_BF16X3, _lib.RMD_S24, 0.0625).dtype == torch.float32
         with pytest.raises(ValueError, match="tiles layout"):
             torch.ops.rmd.corr_lookup(pyr.view(-1, 16), co, 4, 4, 0)
         f = torch.empty(2, 32, 12, 16, device="cuda")

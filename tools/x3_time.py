@@ -37,6 +37,9 @@ def main():
             ts.append(ev[0][0].elapsed_time(ev[0][1]))
     ts.sort()
     data = pyr.data if hasattr(pyr, "data") else pyr
+    if data.dtype == torch.uint8:                 # RMD_S24 bytes
+        from rmd import library
+        data = library.s24_decode(data)
     res.update({"median_ms": ts[len(ts) // 2], "min_ms": ts[0],
                 "checksum": float(data.double().abs().sum()), "nan": bool(torch.isnan(data).any())})
     print(json.dumps(res))
