@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--radius", type=int, default=4)
     ap.add_argument("--levels", type=int, default=4)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32-f32", "fp32-exact", "bf16-f32", "fp32-f16"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32-f32", "fp32-s24", "fp32-exact", "bf16-f32", "fp32-f16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
     ap.add_argument("--event-every", type=int, default=5,
@@ -779,7 +779,7 @@ def rooflines(args, precision, B, h8, w8, gemm_ms, look_ms, traffic, traffic_not
     gemm_bytes = B * N * sum(h * w for h, w in levels) * s + 2 * B * N * args.channels * op_bytes
     gemm_flop = 2.0 * B * N * N * args.channels
     # MFMA work actually issued: the fp32 mode runs three bf16 products per k-step (x3 kernel)
-    mfma_dt, mfma_mult = ("bf16", 3.0) if precision in ("fp32", "fp32-f32") else (compute_dt, 1.0)
+    mfma_dt, mfma_mult = ("bf16", 3.0) if precision in ("fp32", "fp32-f32", "fp32-s24") else (compute_dt, 1.0)
     look_gbs = look_bytes / (look_ms * 1e-3) / 1e9
     gemm_gbs = gemm_bytes / (gemm_ms * 1e-3) / 1e9
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12

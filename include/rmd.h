@@ -57,7 +57,8 @@ extern "C" {
  * with tiles_y[l] = ceil(level_h[l] / tile_h[l]), tiles_x[l] = ceil(level_w[l] / tile_w[l]) and
  * p = y1*W + x1 the query pixel.  Two layouts (`layout`):
  *
- *  RMD_LAYOUT_ROWS  (every GEMM except w8): chunks 1 x (8, 8, 4, 2), slot(p) = p, query_slots = H*W.
+ *  RMD_LAYOUT_ROWS  (every GEMM except w8): chunks 1 x (8, 8, 4, 2) (RMD_S24 storage: 1 x (8, 8, 4, 4),
+ *    so every S24 chunk is a multiple of 4 bytes), slot(p) = p, query_slots = H*W.
  *  RMD_LAYOUT_TILES (the w8 GEMM: bf16 compute, fp16 storage): chunks 2x4, 2x4, 1x4, 1x2 and query
  *    slots in 2 x 16 query tiles whose 8-slot groups are 2 x 4 query patches:
  *      y1 < 2*floor(H/2): slot = ((y1/2)*QX + x1/16)*32 + ((x1%16)/4)*8 + (y1%2)*4 + x1%4, QX = ceil(W/16)

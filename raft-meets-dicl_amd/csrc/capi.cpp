@@ -72,7 +72,8 @@ extern "C" int rmd_pyramid_describe_layout(int batch, int height, int width, int
             return RMD_ERR_SHAPE;
         }
         const int th = tiles && l <= 1 ? 2 : 1;
-        const int tw = tiles ? (l <= 2 ? 4 : 2) : rmd::level_chunk(l);
+        // S24 level 3: 1 x 4 chunks (12 bytes: one 4-aligned load) instead of 1 x 2
+        const int tw = tiles ? (l <= 2 ? 4 : 2) : (storage == RMD_S24 && l == 3 ? 4 : rmd::level_chunk(l));
         d->level_h[l] = h;
         d->level_w[l] = w;
         d->tile_h[l] = th;

@@ -112,6 +112,11 @@ __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, in
 // per-image level slab is below 2^31 bytes.
 constexpr unsigned kOOB = 0x80000000u;
 
+// S24 level-0/1 chunk loads: 0 = two 12-byte loads (product), 1 = 16 + 8 bytes (A/B)
+#ifndef RMD_LOOKUP_S24LD
+#define RMD_LOOKUP_S24LD 0
+#endif
+
 // A/B ablation builds only (tools/build_variant.sh): bit 0 drops the output stores, bit 1 the pyramid
 // loads, by sending them to kOOB (same instruction stream, no memory traffic).  0 in the product.
 #ifndef RMD_LOOKUP_ABL
@@ -170,26 +175,33 @@ __device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_r
     }
 }
 
-// One S24 chunk of CW elements (3 CW bytes at byte offset off of the slab; a = the slab base address
-// mod 4) -> CW fp32 words.  8 / 4 elements: 12-byte loads (4-aligned: level offsets and slot strides are
-// multiples of 4 bytes there).  2 elements (level 3, 6 bytes, 2-aligned): a naturally aligned word +
-// short pair chosen by the address parity — no load reaches outside the chunk, so the slab bound and
-// kOOB zeros stay exact.
+// One S24 chunk of CW = 8 or 4 elements (3 CW bytes at byte offset off of the slab, 4-aligned: level
+// offsets, slot strides and chunk strides are multiples of 12 bytes) -> CW fp32 words: 12-byte loads,
+// each 3 words widened with v_perm.
 template <int CW>
-__device__ __forceinline__ void buf_s24(unsigned (&dst)[CW], __amdgpu_buffer_rsrc_t rs, unsigned off, unsigned a) {
+__device__ __forceinline__ void buf_s24(unsigned (&dst)[CW], __amdgpu_buffer_rsrc_t rs, unsigned off) {
+    static_assert(CW == 8 || CW == 4, "S24 chunks are 1 x 8 or 1 x 4");
     if constexpr ((RMD_LOOKUP_ABL & 2) != 0) off = kOOB;
-    if constexpr (CW == 2) {
-        const bool odd = ((off + a) & 2u) != 0;
-        const unsigned w = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(odd ? off + 2u : off), 0, 0);
-        const unsigned h = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(odd ? off : off + 4u), 0, 0);
-        // even: bytes 0-3 = w, 4-5 = h; odd: bytes 0-1 = h, 2-5 = w
-        dst[0] = odd ? (h << 8) | (w << 24) : w << 8;
-        dst[1] = odd ? w & 0xffffff00u : ((w >> 24) << 8) | (h << 16);
-    } else {
+    {
+        unsigned w[3 * CW / 4];
+        if constexpr (CW == 8 && RMD_LOOKUP_S24LD) {
+            // A/B: 16 + 8 bytes (the chunk is 8-aligned) instead of 2 x 12
+            const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+            const auto b = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(off + 16u), 0, 0);
+            w[0] = (unsigned)a[0]; w[1] = (unsigned)a[1]; w[2] = (unsigned)a[2]; w[3] = (unsigned)a[3];
+            w[4] = (unsigned)b[0]; w[5] = (unsigned)b[1];
+        } else {
+#pragma unroll
+            for (int k = 0; k < CW / 4; ++k) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
+                w[3 * k] = (unsigned)v[0];
+                w[3 * k + 1] = (unsigned)v[1];
+                w[3 * k + 2] = (unsigned)v[2];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < CW / 4; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
-            const unsigned w0 = (unsigned)v[0], w1 = (unsigned)v[1], w2 = (unsigned)v[2];
+            const unsigned w0 = w[3 * k], w1 = w[3 * k + 1], w2 = w[3 * k + 2];
             dst[4 * k + 0] = w0 << 8;
             dst[4 * k + 1] = __builtin_amdgcn_perm(w1, w0, 0x0504030Cu);
             dst[4 * k + 2] = __builtin_amdgcn_perm(w2, w1, 0x0403020Cu);
@@ -300,12 +312,12 @@ __device__ __forceinline__ bool level_setup(const PyrGeom& g, int L, float x, fl
 // edge (MASK; a chunk there holds padding columns).  Rows off the level are whole chunks off the level.
 // S24 chunks are widened to fp32 words as they arrive and then shifted like an f32 level.
 template <typename T, int R, int L, int PR, bool MASK>
-__device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, unsigned a, const PyrGeom& g, int slot, int N,
+__device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, const PyrGeom& g, int slot, int N,
                                               float fx, float fy, int xs, int ys, const OutBuf& ob, int own0, int bb0) {
     constexpr bool S24 = kIsS24<T>;
     using TE = typename std::conditional<S24, float, T>::type;     // element type of the loaded words
     constexpr int D = 2 * R + 1, K = 2 * R + 2, KR = PR + 1;
-    constexpr int CW = level_chunk(L);                              // 8, 8, 4, 2 elements
+    constexpr int CW = S24 && L == 3 ? 4 : level_chunk(L);          // 8, 8, 4, 2 elements (S24: 8, 8, 4, 4)
     constexpr int CB = CW * (int)sizeof(T);                         // chunk bytes
     constexpr int CWW = S24 ? CW : CB / 4;                          // chunk words (S24: widened)
     constexpr int NC = (K + CW - 1 + CW - 1) / CW;                  // chunks a row can span
@@ -328,7 +340,7 @@ __device__ __forceinline__ void rows_body_buf(__amdgpu_buffer_rsrc_t rs, unsigne
             const bool valid = rv && tc >= 0 && tc < txs && c * CW < sh + K;
             unsigned tmp[CWW];
             if constexpr (S24)
-                buf_s24<CW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB, a);
+                buf_s24<CW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB);
             else
                 buf_words<CWW>(tmp, rs, valid ? roff + (unsigned)c * cs : kOOB);
 #pragma unroll
@@ -361,11 +373,10 @@ __device__ __forceinline__ void lookup_level_rows(const T* __restrict__ pyr, con
     const int lh = g.lh[L], lw = g.lw[L];
     if constexpr (BUF) {
         const __amdgpu_buffer_rsrc_t rs = level_rsrc(pyr, g, L, b);
-        const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)level_base(pyr, g, L, b)) & 3u;
         if (__any(xs + K > lw))
-            rows_body_buf<T, R, L, PR, true>(rs, a, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+            rows_body_buf<T, R, L, PR, true>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
         else
-            rows_body_buf<T, R, L, PR, false>(rs, a, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
+            rows_body_buf<T, R, L, PR, false>(rs, g, slot, N, fx, fy, xs, ys, ob, own0, bb0);
         return;
     } else {
         static_assert(!kIsS24<T>, "S24 pyramids are read through buffer loads only");

@@ -624,10 +624,11 @@ __device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (
         t3 += __shfl_xor(t3, 16);
         const float v3 = (1.0f / 64.0f) * t3;
         if constexpr (S24) {
-            // lane g = 0 takes col 1 from lane + 32 and writes the 6-byte chunk as an aligned word + short
+            // lane g = 0 takes col 1 from lane + 32 and writes the block's 6-byte half of the 12-byte chunk as
+            // a naturally aligned word + short
             const float w1 = __shfl_xor(v3, 32);
             const unsigned r0 = s24_round(v3), r1 = s24_round(w1);
-            const unsigned base = q * 2u * E + soff(L[3], 0, 0);       // 2-aligned (chunks are 6 bytes)
+            const unsigned base = q * 12u + soff(L[3], 0, 0);          // 1 x 4 chunks: 2-aligned half chunk
             const bool odd = ((base + L[3].a) & 2u) != 0;
             // even: word = bytes 0-3, short = bytes 4-5; odd: short = bytes 0-1, word = bytes 2-5
             const unsigned word = odd ? __builtin_amdgcn_perm(r1, r0, 0x07060503u) : __builtin_amdgcn_perm(r1, r0, 0x05030201u);
@@ -696,13 +697,15 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
         const int span = kBlockRows >> l, nch = l == 0 ? 2 : 1;
-        const int y0 = rb * span, xc0 = cb * nch;
+        // S24 level 3: 1 x 4 chunks, two blocks per chunk (this block's 2 columns at byte 6 (cb & 1))
+        const bool c4 = S24 && l == 3;
+        const int y0 = rb * span, xc0 = c4 ? cb >> 1 : cb * nch;
         const bool lv = l < g.levels;
         const int cw = g.tw[l];
         const int rows = lv ? max(0, min(span, g.ty[l] - y0)) : 0;
         const unsigned rs = lv ? (unsigned)g.tx[l] * (unsigned)N * cw * E : 0u;
         const size_t base = lv ? ((size_t)g.off[l] + (((size_t)b * g.ty[l] + y0) * g.tx[l] + xc0) * N * cw) : 0;
-        unsigned char* bp = pyr + base * E;
+        unsigned char* bp = pyr + base * E + (c4 && lv ? 6u * (cb & 1) : 0u);
         const unsigned lo32 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)bp);
         const unsigned hi32 = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)bp >> 32));
         L[l].rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uintptr_t)hi32 << 32) | lo32), (short)0,

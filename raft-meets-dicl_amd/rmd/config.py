@@ -26,12 +26,12 @@ values.
 import re
 from collections import namedtuple
 
-PRECISIONS = ("fp32", "fp32-f32", "fp32-exact", "bf16", "bf16-f32", "fp32-f16")
+PRECISIONS = ("fp32", "fp32-f32", "fp32-s24", "fp32-exact", "bf16", "bf16-f32", "fp32-f16")
 METHODS = ("auto", "volume", "otf")
 KEYS = ("corr-precision", "corr-method", "corr-memory-budget")
 DEFAULTS = {"corr-precision": "fp32", "corr-method": "auto", "corr-memory-budget": 16 << 30}
 
-_STORAGE_BYTES = {"fp32": 3, "fp32-f32": 4, "fp32-exact": 4, "bf16": 2, "bf16-f32": 4, "fp32-f16": 2}
+_STORAGE_BYTES = {"fp32": 3, "fp32-f32": 4, "fp32-s24": 3, "fp32-exact": 4, "bf16": 2, "bf16-f32": 4, "fp32-f16": 2}
 
 
 class CorrOptions(namedtuple("CorrOptions", ["precision", "method", "memory_budget"])):

@@ -18,6 +18,7 @@ from ._lib import RMD_BF16, RMD_BF16X3, RMD_F16, RMD_F32, RMD_S24
 PRECISIONS = {
     "fp32": (RMD_BF16X3, RMD_S24),    # fp32-accurate split-bf16 MFMA (3 products), 24-bit pyramid: parity mode (default)
     "fp32-f32": (RMD_BF16X3, RMD_F32),# the same GEMM, f32 pyramid
+    "fp32-s24": (RMD_BF16X3, RMD_S24),# the same GEMM, 24-bit pyramid
     "fp32-exact": (RMD_F32, RMD_F32), # exact f32 MFMA (v_mfma_f32_32x32x2_f32), f32 pyramid
     "bf16": (RMD_BF16, RMD_F16),      # bf16 MFMA operands, f32 accumulate, fp16 pyramid: perf mode
     "bf16-f32": (RMD_BF16, RMD_F32),  # bf16 operands, f32 pyramid

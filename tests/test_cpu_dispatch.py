@@ -71,20 +71,25 @@ def test_s24_encoding_rounds_half_away_and_keeps_specials():
 
 
 def test_cpu_lookup_reads_s24_pyramids():
-    """An S24 pyramid (uint8 (n, 3), the x3 GEMM's output) looked up on the CPU equals the lookup of
-    its decoded f32 values; its shape and dtype carry the storage."""
+    """An S24 pyramid (uint8 (n, 3), the x3 GEMM's output format: 1 x (8, 8, 4, 4) chunks) looked up on
+    the CPU: its shape and dtype carry the storage, and the result is the reference's within the
+    2^-16 relative rounding of the stored values."""
     import rmd
+    from rmd import _lib, cpu, library
     g = load_golden("corr_b2_c32_24x40")
     f1, f2, co = _t(g["fmap1"]), _t(g["fmap2"]), _t(g["coords"])
     lv, r = int(g["levels"]), int(g["radius"])
-    p32 = torch.ops.rmd.corr_pyramid(f1, f2, lv, rmd._lib.RMD_BF16X3, rmd._lib.RMD_S24, 1.0 / 32 ** 0.5)
+    b, c, h, w = f1.shape
+    p32 = torch.ops.rmd.corr_pyramid(f1, f2, lv, _lib.RMD_BF16X3, _lib.RMD_S24, 1.0 / c ** 0.5)
     assert p32.dtype == torch.float32 and p32.dim() == 1          # the CPU GEMM stores F32
-    p24 = rmd.library.s24_encode(p32)
-    assert p24.dtype == torch.uint8 and p24.shape == (p32.numel(), 3)
-    assert rmd.library.pyramid_storage(p24) == rmd._lib.RMD_S24
+    d24 = _lib.describe(b, h, w, lv, _lib.RMD_S24)
+    assert d24.tile_w[lv - 1] == (4 if lv == 4 else d24.tile_w[lv - 1])
+    p24 = library.s24_encode(cpu._pack_rows(cpu._corr_levels(f1, f2, lv, 1.0 / c ** 0.5), d24, torch.float32))
+    assert p24.dtype == torch.uint8 and p24.shape == (d24.total_elements, 3)
+    assert library.pyramid_storage(p24) == _lib.RMD_S24
     a = torch.ops.rmd.corr_lookup(p24, co, lv, r, 0)
-    b = torch.ops.rmd.corr_lookup(rmd.library.s24_decode(p24), co, lv, r, 0)
-    assert torch.equal(a, b)
+    ref = torch.ops.rmd.corr_lookup(p32, co, lv, r, 0)
+    assert rel_max_err(a.numpy(), ref.numpy()) < 2e-5
     assert rel_max_err(a.numpy(), g["out"]) < 2e-5
 
 

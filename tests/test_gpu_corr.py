@@ -477,23 +477,27 @@ def test_s24_pyramid_is_rounded_f32_pyramid(c, b, h, w):
     """The x3 GEMM's S24 epilogue (fp32 mode) against its F32 epilogue (fp32-f32) on the same inputs:
     every stored element equals the F32 value rounded by the RMD_S24 rule (rmd.library.s24_encode),
     bit for bit — all four levels, odd / even query parity of the 6-byte level-3 chunks, ragged maps and
-    C < 256 — and the lookup of the S24 pyramid equals the lookup of its decoded f32 values."""
+    C < 256 — and the lookup of the S24 pyramid equals the lookup of the rounded values in an F32 pyramid."""
     import rmd
     from rmd import _lib, library
     rng = np.random.default_rng(c * 7 + h * w + b)
     f1 = rng.standard_normal((b, c, h, w)).astype(np.float32)
     f2 = rng.standard_normal((b, c, h, w)).astype(np.float32)
     f1[0, :, 0, 0] = np.nan                                         # a NaN query row stays NaN
-    p24 = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "fp32")
+    p24 = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "fp32-s24")
     p32 = rmd.ops.corr_pyramid(_t(f1), _t(f2), 4, "fp32-f32")
     assert p24.desc.storage == _lib.RMD_S24 and p24.data.dtype == torch.uint8
-    assert p24.data.shape == (p32.desc.total_elements, 3)
-    enc = library.s24_encode(p32.data)
-    assert torch.equal(p24.data, enc)
+    assert p24.data.shape == (p24.desc.total_elements, 3)
+    assert p24.desc.tile_w[3] == 4                                  # S24 level 3: 1 x 4 chunks
+    for i in range(4):
+        got = p24.unpack(i).reshape(-1)
+        ref = library.s24_decode(library.s24_encode(p32.unpack(i)))
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), f"level {i}"
     ys, xs = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
     co = _t((np.stack([xs, ys])[None] + rng.normal(0, 3, (b, 2, h, w))).astype(np.float32))
     a = torch.ops.rmd.corr_lookup(p24.data, co, 4, 4, 0)
-    r = torch.ops.rmd.corr_lookup(library.s24_decode(p24.data), co, 4, 4, 0)
+    # the F32 pyramid rounded in place (F32 layout, the S24 values): the same lookup arithmetic
+    r = torch.ops.rmd.corr_lookup(library.s24_decode(library.s24_encode(p32.data)), co, 4, 4, 0)
     assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(r, nan=7.0))
 
 
