@@ -112,11 +112,6 @@ __device__ __forceinline__ void shift_extract(unsigned (&wd)[NW + 1], int sh, in
 // per-image level slab is below 2^31 bytes.
 constexpr unsigned kOOB = 0x80000000u;
 
-// S24 level-0/1 chunk loads: 0 = two 12-byte loads (product), 1 = 16 + 8 bytes (A/B)
-#ifndef RMD_LOOKUP_S24LD
-#define RMD_LOOKUP_S24LD 0
-#endif
-
 // A/B ablation builds only (tools/build_variant.sh): bit 0 drops the output stores, bit 1 the pyramid
 // loads, by sending them to kOOB (same instruction stream, no memory traffic).  0 in the product.
 #ifndef RMD_LOOKUP_ABL
@@ -183,21 +178,14 @@ __device__ __forceinline__ void buf_s24(unsigned (&dst)[CW], __amdgpu_buffer_rsr
     static_assert(CW == 8 || CW == 4, "S24 chunks are 1 x 8 or 1 x 4");
     if constexpr ((RMD_LOOKUP_ABL & 2) != 0) off = kOOB;
     {
+        // (16 + 8-byte loads of the 8-aligned level-0/1 chunks measured the same, profiles/s24_ab_r05.json)
         unsigned w[3 * CW / 4];
-        if constexpr (CW == 8 && RMD_LOOKUP_S24LD) {
-            // A/B: 16 + 8 bytes (the chunk is 8-aligned) instead of 2 x 12
-            const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-            const auto b = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(off + 16u), 0, 0);
-            w[0] = (unsigned)a[0]; w[1] = (unsigned)a[1]; w[2] = (unsigned)a[2]; w[3] = (unsigned)a[3];
-            w[4] = (unsigned)b[0]; w[5] = (unsigned)b[1];
-        } else {
 #pragma unroll
-            for (int k = 0; k < CW / 4; ++k) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
-                w[3 * k] = (unsigned)v[0];
-                w[3 * k + 1] = (unsigned)v[1];
-                w[3 * k + 2] = (unsigned)v[2];
-            }
+        for (int k = 0; k < CW / 4; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
+            w[3 * k] = (unsigned)v[0];
+            w[3 * k + 1] = (unsigned)v[1];
+            w[3 * k + 2] = (unsigned)v[2];
         }
 #pragma unroll
         for (int k = 0; k < CW / 4; ++k) {
@@ -534,10 +522,9 @@ __device__ __forceinline__ void lookup_level_tiles(const __half* __restrict__ py
     }
 }
 
-// grid: (slot blocks of 64, batch, level + levels * part) — one lane per (query slot, level, row part)
-#ifndef RMD_LOOKUP_ZORD
-#define RMD_LOOKUP_ZORD 0
-#endif
+// grid: (slot blocks of 64, batch, level + levels * part) — one lane per (query slot, level, row part).
+// (Row parts adjacent in dispatch order, one XCD apart, and level 0 last measured no gain,
+// profiles/lookup_order_ab_r05.json.)
 #ifndef RMD_LOOKUP_WPE8
 #define RMD_LOOKUP_WPE8 0
 #endif
@@ -551,19 +538,9 @@ __global__ void __launch_bounds__(kThreads) RMD_LOOKUP_ATTR
 corr_lookup_kernel(const T* __restrict__ pyr, PyrGeom g, const float* __restrict__ coords, unsigned zmask,
                    float* __restrict__ out) {
     const int N = g.height * g.width;
-#if RMD_LOOKUP_ZORD
-    // A/B: the 3 row parts of a slot block 8 blocks apart (one XCD under round-robin dispatch), one
-    // level per z (ZORD 2: level 0 last)
-    const int grp = (int)blockIdx.x / 24, rem = (int)blockIdx.x - grp * 24;
-    const int part = rem >> 3;
-    const int s = (grp * 8 + (rem & 7)) * kThreads + threadIdx.x;
-    if ((grp * 8 + (rem & 7)) * kThreads >= g.slots) return;
-    const int L = RMD_LOOKUP_ZORD == 2 ? g.levels - 1 - (int)blockIdx.z : (int)blockIdx.z;
-#else
     const int s = blockIdx.x * kThreads + threadIdx.x;
     const int L = (int)blockIdx.z % g.levels;
     const int part = (int)blockIdx.z / g.levels;
-#endif
     const int b = blockIdx.y;
     bool active;
     int p, slot;
@@ -612,11 +589,7 @@ template <typename T, int LAY>
 int launch_lookup(const void* pyr, const rmd_pyramid_desc& d, const float* coords, int radius, unsigned zmask,
                   float* out, hipStream_t st) {
     const PyrGeom g = make_geom(d);
-#if RMD_LOOKUP_ZORD
-    const dim3 grid(((g.slots + kThreads - 1) / kThreads + 7) / 8 * 24, d.batch, d.levels);
-#else
     const dim3 grid((g.slots + kThreads - 1) / kThreads, d.batch, d.levels * 3);
-#endif
     const T* p = reinterpret_cast<const T*>(pyr);
     // buffer loads need every per-image level slab below 2^31 bytes (kOOB must lie past it); the
     // pointer path stays for larger pyramids (-DRMD_LOOKUP_BUF=0 forces it for A/B builds)
