@@ -538,6 +538,8 @@ __device__ __forceinline__ void ksteps16(f32x4 (&acc)[8][2], bf16x8 (&acur)[8], 
             rl[slot][M] = *reinterpret_cast<const bf16x8*>(p + lo_off);
         }
         const f32x4 zero = {};
+        // (product-outer order, 8 independent accumulators between dependent MFMAs: same cycles,
+        // profiles/x3_ab_r05.json ord1)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
