@@ -68,6 +68,18 @@ def test_describe_for_w8_tiles_layout_geometry():
         _lib.describe(1, 8, 8, 2, _lib.RMD_F32, _lib.RMD_LAYOUT_TILES)     # tiles are fp16 only
 
 
+def test_describe_for_x3_s24_geometry():
+    """The x3 GEMM (split-bf16 compute) writes S24 pyramids in the row layout with 1 x 4 level-3 chunks;
+    an S24 request another GEMM serves (C > 256, exact f32) resolves to F32 rows."""
+    from rmd import _lib
+    d = _lib.describe_for(8, 55, 128, 4, _lib.RMD_S24, 256, _lib.RMD_BF16X3)
+    assert d.storage == _lib.RMD_S24 and d.layout == _lib.RMD_LAYOUT_ROWS
+    assert [d.tile_w[i] for i in range(4)] == [8, 8, 4, 4]
+    for c, compute in ((320, _lib.RMD_BF16X3), (256, _lib.RMD_F32)):
+        r = _lib.describe_for(8, 55, 128, 4, _lib.RMD_S24, c, compute)
+        assert r.storage == _lib.RMD_F32 and r.layout == _lib.RMD_LAYOUT_ROWS
+
+
 @pytest.mark.parametrize("h,w", [(55, 128), (46, 62), (9, 17), (1, 40), (48, 160)])
 def test_tiles_slots_are_a_padded_bijection(h, w):
     """rmd.ops.tiles_slots (the unpack map) is injective, stays below query_slots, and every 8-slot

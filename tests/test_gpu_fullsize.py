@@ -111,8 +111,9 @@ def test_dap_b8_full_size(d, h, w):
 def test_cfg2_whole_volume_across_gemm_kernels():
     """cfg2 (B=8, 55x128, C=256) whole volume, every level and a whole lookup output, across three
     independent GEMM kernels (each pinned to the oracle on samples in test_gpu_corr.py):
-      * fp32 parity mode (corr_pyramid_x3, split-bf16 MFMA, row layout) vs fp32-exact
-        (corr_pyramid_tiled, exact f32 MFMA): max|d| / max|ref| <= 1e-4 (north_star fp32 gate);
+      * fp32 parity mode (corr_pyramid_x3s, split-bf16 MFMA, S24 row layout) and fp32-f32 (the same GEMM,
+        F32 row layout) vs fp32-exact (corr_pyramid_tiled, exact f32 MFMA): max|d| / max|ref| <= 1e-4
+        (north_star fp32 gate);
       * bf16 perf mode (corr_pyramid_w8, tiles layout, fp16 storage) vs fp32-exact: <= 1e-2.
     1.3e10 pyramid values per mode are compared on the GPU (no oracle can run at this size)."""
     import rmd
@@ -126,7 +127,7 @@ def test_cfg2_whole_volume_across_gemm_kernels():
     co = (torch.stack([xs, ys])[None] + flow + torch.randn(b, 2, 1, 1, generator=g) * 4.0).to(DEV)
     ref = rmd.ops.corr_pyramid(f1, f2, 4, "fp32-exact")
     out_ref = rmd.ops.corr_lookup(ref, co, 4)
-    for precision, tol, layout in (("fp32", 1e-4, 0), ("bf16", 1e-2, 1)):
+    for precision, tol, layout in (("fp32", 1e-4, 0), ("fp32-f32", 1e-4, 0), ("bf16", 1e-2, 1)):
         pyr = rmd.ops.corr_pyramid(f1, f2, 4, precision)
         assert pyr.desc.layout == layout
         for i in range(4):
