@@ -8,7 +8,7 @@ The correlation blocks it then constructs take only ``(fmap1, fmap2, num_levels,
 section; all are optional and their defaults reproduce the reference:
 
   corr-precision      fp32 (default: split-bf16 MFMA, 24-bit pyramid (fp32 rounded to 16 significant
-                      bits), ~1e-5 of the reference) | fp32-f32 (same GEMM, fp32 pyramid) |
+                      bits), ~1e-5 of the reference) | fp32-f32 (same GEMM, fp32 pyramid) | fp32-s24 (= fp32) |
                       fp32-exact | bf16 (bf16 MFMA, fp16 pyramid: the bench mode) | bf16-f32 | fp32-f16
   corr-method         auto (default) | volume | otf — all-pairs pyramid + lookup, or the on-the-fly
                       lookup with no O(N^2) buffer (both differentiable); auto takes the volume unless
