@@ -219,6 +219,17 @@ long long rmd_corr_grad_targets(int height, int width, int levels);
 int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid_desc* desc, const float* coords,
                              int radius, unsigned zero_level_mask, float* grad_levels, void* stream);
 
+/* G of ALL nlookups lookups of one forward in one pass: grad_levels = (accumulate ? G : 0)
+ * + sum over i in order of lookup i's contribution (grad_outs[i], coords[i], zero_level_masks[i] —
+ * each as in rmd_corr_lookup_backward; masks may be NULL), writing every element of G (no zero fill
+ * needed).  Same arithmetic and summation order as the sequence of rmd_corr_lookup_backward calls
+ * i = 0, 1, ... into a zeroed G.  grad_outs / coords / zero_level_masks are HOST arrays of device
+ * pointers / values.  Replaces the per-lookup grid_sampler_2d_backward of raft.py:80 plus the
+ * accumulation of those gradients into the correlation volume that autograd performs. */
+int rmd_corr_grad_build(const float* const* grad_outs, const float* const* coords,
+                        const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* desc, int radius,
+                        int accumulate, float* grad_levels, void* stream);
+
 /* pooled (B, C, T') = avg_pool_{2^l}(fmap2) * scale for every level, in G's padded target order (pad
  * targets 0) (raft.py:35-47 applied to the feature map, which commutes with the product). */
 int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,

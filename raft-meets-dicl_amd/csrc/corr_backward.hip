@@ -67,6 +67,10 @@ inline GradGeom make_grad_geom(int batch, int h, int w, int levels) {
     return g;
 }
 
+// a (1 - f) + b f as one explicit fma over a rounded product: both G kernels (sequential and build)
+// then round identically whatever the compiler's contraction choices (bit-equal G)
+__device__ __forceinline__ float xlerp(float a, float b, float f) { return __builtin_fmaf(a, 1.0f - f, b * f); }
+
 // grid: (query blocks of 64, batch, level + levels * part); one lane per (query, level, part), part k
 // producing patch rows [k*PR, min(K, (k+1)*PR)) from tap rows k*PR - 1 .. (k+1)*PR - 1
 constexpr int kBwdThreads = 64, kBwdParts = 3;
@@ -105,7 +109,7 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
 #pragma unroll
             for (int a = 0; a < D; ++a) gr[a] = go[(size_t)(a * D + j) * N];   // channel a*D + j
 #pragma unroll
-            for (int i = 0; i < K; ++i) q[i] = (i < D ? gr[i] * (1.0f - fx) : 0.f) + (i >= 1 ? gr[i - 1] * fx : 0.f);
+            for (int i = 0; i < K; ++i) q[i] = xlerp(i < D ? gr[i] : 0.f, i >= 1 ? gr[i - 1] : 0.f, fx);
         } else {
 #pragma unroll
             for (int i = 0; i < K; ++i) q[i] = 0.f;
@@ -132,7 +136,7 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
                 constexpr int NC = (K + 14) / 8, NW = 8 * NC;
                 float wv[NW];
 #pragma unroll
-                for (int i = 0; i < NW; ++i) wv[i] = i < K ? qcur[i] * (1.0f - fy) + qprev[i] * fy : 0.f;
+                for (int i = 0; i < NW; ++i) wv[i] = i < K ? xlerp(qcur[i], qprev[i], fy) : 0.f;
                 const int sh = xs & 7;
 #pragma unroll
                 for (int st = 1; st < 8; st <<= 1) {
@@ -170,6 +174,247 @@ corr_lookup_backward_kernel(const float* __restrict__ gout, GradGeom g, const fl
         }
 #pragma unroll
         for (int i = 0; i < K; ++i) qprev[i] = qcur[i];
+    }
+}
+
+// ---- G build: every lookup of a forward in one pass that writes G once -------------------------
+//
+// rmd_corr_grad_build replaces (zero-fill G) + (one rmd_corr_lookup_backward per lookup): 2.09 GB
+// of zeros plus 12 read-modify-write passes (0.35 + 12 x 0.065 ms at cfg2 b8) become one write of G.
+// One wave per segment = (image b, 64 consecutive queries, level L, kBuildSegRows target rows,
+// kBuildChunks chunk columns); lane = query p.  The lanes' patch origins for every lookup are staged in
+// LDS once per segment; the segment's target rows are then built kBuildRows at a time in an LDS tile
+// laid out [row][slot][query] (slot = a target column of the tile, plus a trash slot at each end), so
+// a lane adds its patch values at per-lane columns without bank conflicts, shifts or selects.
+// Lookups go in groups of kBuildGroup: a lane whose (2r+2)^2 patch meets the tile loads its
+// coordinates and the kBuildRows + 1 tap rows it needs, for the whole group in one batch of buffer
+// loads (tap rows outside 0 .. 2r, and lanes / lookups that miss the tile, go to an out-of-range
+// offset: zeros, no traffic); it forms the patch rows with the x-then-y bilinear arithmetic of
+// corr_lookup_backward_kernel (xlerp) and adds them into the tile in lookup order.  Columns left or
+// right of the tile land in the trash slots.  The wave then stores the tile — lane l writes the 16 B
+// at byte 16 l of each 1-KB half of a (row, chunk)'s 2 KB, read across lanes, so every store
+// instruction covers 8 whole 128-B lines, non-temporal (G is 2 GB, read next by the GEMMs) — with pad
+// targets x >= W_l as 0, and clears it.  Each G element thus receives 0 + v_0 + v_1 + ... in lookup
+// order: the sum the sequential kernels form, bit for bit.  ACC: a tile starts from G's current
+// values (launches after the first when a forward holds more than kBuildMax lookups).
+// Measured variants (profiles/grad_build_r05.json): register tiles with select-shifted accumulation,
+// one unit per wave, 1-row / 4-row tiles, lookup-at-a-time loads, a producer / consumer wave pair.
+#ifndef RMD_BUILD_ROWS
+#define RMD_BUILD_ROWS 2
+#endif
+#ifndef RMD_BUILD_CHUNKS
+#define RMD_BUILD_CHUNKS 4
+#endif
+// 1: G stores non-temporal (streamed past L2, which then keeps the grad_out / coordinate reads)
+#ifndef RMD_BUILD_NT
+#define RMD_BUILD_NT 1
+#endif
+// A/B ablations only: bit 0 sends every grad_out load out of range (no memory traffic, zeros)
+#ifndef RMD_BUILD_ABL
+#define RMD_BUILD_ABL 0
+#endif
+#ifndef RMD_BUILD_SEG
+#define RMD_BUILD_SEG 8
+#endif
+constexpr int kBuildMax = 16, kBuildRows = RMD_BUILD_ROWS, kBuildChunks = RMD_BUILD_CHUNKS, kBuildThreads = 64;
+constexpr int kBuildSegRows = RMD_BUILD_SEG * kBuildRows;     // target rows per wave (tiles in sequence)
+#ifndef RMD_BUILD_GROUP
+#define RMD_BUILD_GROUP 4
+#endif
+constexpr int kBuildGroup = RMD_BUILD_GROUP;                 // lookups per batch of loads
+constexpr int kBuildSlots = 8 * kBuildChunks + 2;            // tile columns + 2 trash slots
+constexpr unsigned kBuildOOB = 0x80000000u;                  // buffer offset past any slab: loads return 0
+
+struct BuildArgs {
+    const float* gout[kBuildMax];
+    const float* coords[kBuildMax];
+    unsigned zmask[kBuildMax];
+    int n;                              // lookups in this launch (0 .. kBuildMax)
+    int ufirst[RMD_MAX_LEVELS + 1];     // first unit of level l (per image and query block)
+    int nct[RMD_MAX_LEVELS];            // chunk-column tiles of level l
+};
+
+// query coordinate at level L, clamped to +-30000 (beyond it no patch meets a level, H, W < 2^15;
+// the sequential kernel's +-1e6 clamp differs only where neither adds anything)
+__device__ __forceinline__ float build_coord(float c, float inv) { return fminf(fmaxf(c * inv, -30000.f), 30000.f); }
+
+template <int R, bool ACC>
+__global__ void __launch_bounds__(kBuildThreads)
+corr_grad_build_kernel(BuildArgs a, GradGeom g, float* __restrict__ grad) {
+    constexpr int D = 2 * R + 1, K = 2 * R + 2;
+    constexpr int RB = kBuildRows, CB = kBuildChunks, TS = kBuildSlots, TILE = RB * TS * kBuildThreads;
+    __shared__ float tile[TILE];                             // [row][slot][query]
+    __shared__ int sxy[kBuildMax * kBuildThreads];           // [lookup][query] patch origin (xs | ys << 16)
+    const int N = g.height * g.width;
+    const int lane = threadIdx.x;
+    const int p0 = blockIdx.x * kBuildThreads;
+    const int pc = p0 + lane < N ? p0 + lane : N - 1;        // lanes past N compute on a valid query, store nothing
+    const int b = blockIdx.y;
+    int u = blockIdx.z, L = 0;
+    while (L + 1 < g.levels && u >= a.ufirst[L + 1]) ++L;
+    u -= a.ufirst[L];
+    const int lh = g.lh[L], lw = g.lw[L], nch = g.nch[L];
+    const int ys0 = (u / a.nct[L]) * kBuildSegRows, ys1 = min(lh, ys0 + kBuildSegRows);
+    const int clo = (u % a.nct[L]) * CB, ncol = min(nch - clo, CB);
+    const bool lok = lh >= 2 && lw >= 2;                      // 1-pixel levels: NaN in the reference, no gradient
+    const float inv = 1.0f / (float)(1 << L);
+    const size_t chs = (size_t)N * kGcw;                      // one chunk step
+    const int ntile = (ys1 - ys0 + RB - 1) / RB;
+
+    for (int t = lane; t < TILE; t += kBuildThreads) tile[t] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kBuildMax; ++i) {
+        if (i < a.n) {
+            const float* co = a.coords[i] + (size_t)b * 2 * N + pc;
+            const int xs = (int)floorf(build_coord(co[0], inv)) - R, ys = (int)floorf(build_coord(co[N], inv)) - R;
+            sxy[i * kBuildThreads + lane] = (xs & 0xffff) | (ys << 16);
+        }
+    }
+
+    // the segment's tiles in turn (the lookup state above serves all of them): build, store, clear
+    for (int st = 0; st < ntile; ++st) {
+        float* __restrict__ tb = tile;
+        const int y0 = ys0 + st * RB, nr = min(ys1 - y0, RB);
+        {
+            if constexpr (ACC) {
+                const float* col = grad + (((size_t)b * g.TC + g.coff[L]) * N + pc) * kGcw + ((size_t)y0 * nch + clo) * chs;
+#pragma unroll
+                for (int r = 0; r < RB; ++r)
+#pragma unroll
+                    for (int k = 0; k < CB; ++k) {
+                        if (r >= nr || k >= ncol) continue;
+                        const float4* sp = reinterpret_cast<const float4*>(col + ((size_t)r * nch + k) * chs);
+                        const float4 va = sp[0], vb = sp[1];
+                        const float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) tb[(r * TS + 1 + 8 * k + e) * kBuildThreads + lane] = v[e];
+                    }
+            }
+            const unsigned slab = (unsigned)(D * D * N) * 4u;                  // one (b, level) gout block
+            // lookups in groups of BG: the tap rows and coordinates of a whole group are one batch of
+            // loads (lanes / lookups that do not meet the tile load from an out-of-range offset: no
+            // traffic), so a tile waits for memory once per group instead of once per lookup
+            constexpr int BG = kBuildGroup;
+            for (int i0 = 0; i0 < a.n; i0 += BG) {
+                bool act[BG];
+                int xsg[BG], j0g[BG];
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < BG; ++q) {
+                    const int i = i0 + q;
+                    act[q] = false;
+                    xsg[q] = j0g[q] = 0;
+                    if (i < a.n) {
+                        const int xy = sxy[i * kBuildThreads + lane];
+                        const int xs = (int)(short)(xy & 0xffff), ys = xy >> 16;
+                        const int j0 = y0 - ys;             // patch row of tile row 0
+                        const int c0 = xs >> 3, nc = ((xs & 7) + K + 7) >> 3;
+                        const bool on = lok && !((a.zmask[i] >> L) & 1u);
+                        act[q] = on && j0 < K && j0 + nr > 0 && c0 < clo + ncol && c0 + nc > clo;
+                        xsg[q] = xs;
+                        j0g[q] = j0;
+                        any = any || act[q];
+                    }
+                }
+                if (!__any(any)) continue;
+                float gt[BG][RB + 1][D], cxg[BG], cyg[BG];
+#pragma unroll
+                for (int q = 0; q < BG; ++q) {
+                    const int i = i0 + q;
+                    cxg[q] = cyg[q] = 0.f;
+                    if (i >= a.n) continue;
+                    const float* co = a.coords[i] + (size_t)b * 2 * N + pc;
+                    cxg[q] = co[0];
+                    cyg[q] = co[N];
+                    // tap rows j0 - 1 .. j0 + RB - 1 of lookup i, rows outside 0 .. D-1 -> 0
+                    const float* blk = a.gout[i] + ((size_t)b * g.levels + L) * D * D * (size_t)N;
+                    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)blk);
+                    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)blk >> 32));
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo), (short)0, (int)slab, 0x00020000);
+#pragma unroll
+                    for (int r = 0; r <= RB; ++r) {
+                        const int jt = j0g[q] - 1 + r;
+                        const unsigned vo = act[q] && jt >= 0 && jt < D && !(RMD_BUILD_ABL & 1)
+                                                ? (unsigned)(jt * N + pc) * 4u : kBuildOOB;
+#pragma unroll
+                        for (int t = 0; t < D; ++t)
+                            gt[q][r][t] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                rs, (int)vo, (int)__builtin_amdgcn_readfirstlane((unsigned)(t * D * N) * 4u), 0));
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < BG; ++q) {
+                    if (!act[q]) continue;
+                    const float cx = build_coord(cxg[q], inv), cy = build_coord(cyg[q], inv);
+                    const float fx = cx - floorf(cx), fy = cy - floorf(cy);
+                    const int j0 = j0g[q];
+                    float qprev[K];
+#pragma unroll
+                    for (int t = 0; t < K; ++t)
+                        qprev[t] = xlerp(t < D ? gt[q][0][t] : 0.f, t >= 1 ? gt[q][0][t - 1] : 0.f, fx);
+                    const int sb = xsg[q] - 8 * clo + 1;    // tile slot of patch column 0
+#pragma unroll
+                    for (int r = 0; r < RB; ++r) {
+                        float qcur[K];
+#pragma unroll
+                        for (int t = 0; t < K; ++t)
+                            qcur[t] = xlerp(t < D ? gt[q][r + 1][t] : 0.f, t >= 1 ? gt[q][r + 1][t - 1] : 0.f, fx);
+                        const int jr = j0 + r;              // patch row of tile row r
+                        if (r < nr && jr >= 0 && jr < K) {
+                            float* trow = tb + r * TS * kBuildThreads + lane;
+                            float w[K];
+                            int at[K];
+#pragma unroll
+                            for (int t = 0; t < K; ++t) {
+                                at[t] = min(max(sb + t, 0), TS - 1) * kBuildThreads;
+                                w[t] = trow[at[t]];
+                            }
+#pragma unroll
+                            for (int t = 0; t < K; ++t) w[t] += xlerp(qcur[t], qprev[t], fy);
+#pragma unroll
+                            for (int t = 0; t < K; ++t) trow[at[t]] = w[t];
+                        }
+#pragma unroll
+                        for (int t = 0; t < K; ++t) qprev[t] = qcur[t];
+                    }
+                }
+            }
+        }
+        __syncthreads();                                    // (one wave) the tile is read across lanes below
+        {
+            // per (row, chunk) the 64 queries' 32-B pieces are 2 KB contiguous; lane l stores the 16 B at
+            // byte 16 l of each 1-KB half (query 32 h + l / 2, slots 4 (l & 1) ..), so every store
+            // instruction writes 8 whole 128-B lines; the tile is cleared for the next one on the way
+            float* __restrict__ gb = grad + (((size_t)b * g.TC + g.coff[L]) * N + p0) * kGcw +
+                                     ((size_t)y0 * nch + clo) * chs;
+            const int e0 = 4 * (lane & 1);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+#pragma unroll
+                for (int k = 0; k < CB; ++k) {
+                    if (r >= nr || k >= ncol) continue;
+                    const int lim = lw - 8 * (clo + k);     // slots e < lim are on the level (pads stay 0)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int q = 32 * h + (lane >> 1);
+                        float v[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            float* at = tb + (r * TS + 1 + 8 * k + e0 + j) * kBuildThreads + q;
+                            v[j] = e0 + j < lim ? *at : 0.f;
+                            *at = 0.f;
+                        }
+                        if (p0 + q < N) {
+                            typedef __attribute__((ext_vector_type(4))) float f32x4;
+                            f32x4* d = reinterpret_cast<f32x4*>(gb + ((size_t)r * nch + k) * chs + (size_t)q * kGcw + e0);
+                            if constexpr (RMD_BUILD_NT) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, d);
+                            else *d = f32x4{v[0], v[1], v[2], v[3]};
+                        }
+                    }
+                }
+        }
+        __syncthreads();
     }
 }
 
@@ -261,6 +506,61 @@ extern "C" int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid
             return RMD_ERR_SHAPE;
     }
     return rmd::check_launch("rmd_corr_lookup_backward");
+}
+
+extern "C" int rmd_corr_grad_build(const float* const* grad_outs, const float* const* coords,
+                                   const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* d,
+                                   int radius, int accumulate, float* grad_levels, void* stream) {
+    RMD_REQUIRE(d && grad_levels && nlookups >= 0 && (nlookups == 0 || (grad_outs && coords)), RMD_ERR_ARG,
+                "rmd_corr_grad_build: null pointer or negative lookup count");
+    RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_grad_build: radius %d not in 1..8", radius);
+    int rc = rmd::check_grad_args(d->batch, 1, d->height, d->width, d->levels);
+    if (rc) return rc;
+    for (int i = 0; i < nlookups; ++i)
+        RMD_REQUIRE(grad_outs[i] && coords[i], RMD_ERR_ARG, "rmd_corr_grad_build: null pointer (lookup %d)", i);
+    // the kernel clamps coordinates to +-30000 (patch origins in 16 bits) and addresses one (image,
+    // level) block of grad_out with 32-bit buffer offsets
+    RMD_REQUIRE(d->height < 16384 && d->width < 16384, RMD_ERR_SHAPE, "rmd_corr_grad_build: %dx%d map (< 16384)",
+                d->height, d->width);
+    RMD_REQUIRE((long long)(2 * radius + 1) * (2 * radius + 1) * d->height * d->width * 4 < (1LL << 31), RMD_ERR_SHAPE,
+                "rmd_corr_grad_build: grad_out level block >= 2 GiB");
+    const rmd::GradGeom g = rmd::make_grad_geom(d->batch, d->height, d->width, d->levels);
+    const int N = d->height * d->width;
+    rmd::BuildArgs a{};
+    int units = 0;
+    for (int l = 0; l < d->levels; ++l) {
+        a.ufirst[l] = units;
+        a.nct[l] = (g.nch[l] + rmd::kBuildChunks - 1) / rmd::kBuildChunks;
+        units += (g.lh[l] + rmd::kBuildSegRows - 1) / rmd::kBuildSegRows * a.nct[l];
+    }
+    a.ufirst[d->levels] = units;
+    RMD_REQUIRE(units <= 65535 && d->batch <= 65535, RMD_ERR_SHAPE, "rmd_corr_grad_build: %d units x %d images",
+                units, d->batch);
+    const dim3 grid((N + rmd::kBuildThreads - 1) / rmd::kBuildThreads, d->batch, units);
+    hipStream_t st = rmd::as_stream(stream);
+    // one launch per kBuildMax lookups; after the first, each launch adds to G in lookup order
+    for (int i0 = 0; i0 < nlookups || (i0 == 0 && !accumulate); i0 += rmd::kBuildMax) {
+        a.n = nlookups - i0 < rmd::kBuildMax ? nlookups - i0 : rmd::kBuildMax;
+        for (int i = 0; i < a.n; ++i) {
+            a.gout[i] = grad_outs[i0 + i];
+            a.coords[i] = coords[i0 + i];
+            a.zmask[i] = zero_level_masks ? zero_level_masks[i0 + i] : 0u;
+        }
+        const bool acc = accumulate || i0 > 0;
+        switch (radius) {
+#define RMD_CASE(RR)                                                                                              \
+    case RR:                                                                                                      \
+        if (acc) rmd::corr_grad_build_kernel<RR, true><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, grad_levels);   \
+        else rmd::corr_grad_build_kernel<RR, false><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, grad_levels);     \
+        break;
+            RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
+#undef RMD_CASE
+        }
+        rc = rmd::check_launch("rmd_corr_grad_build");
+        if (rc != RMD_OK) return rc;
+        if (nlookups == 0) break;
+    }
+    return RMD_OK;
 }
 
 extern "C" int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,

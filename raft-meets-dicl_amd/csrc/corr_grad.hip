@@ -300,8 +300,18 @@ struct Plan {
 #endif
 inline int tile_n(int Nc) { return RMD_GG_TN == 256 && Nc >= 1024 ? 256 : 128; }
 
-// split count: smallest s minimising (workgroup rounds over 256 CUs) x (K chunks per split), plus a
-// small charge per split for the workspace pass
+// split count: the s minimising (workgroup rounds over 256 CUs) x (K chunks per split) plus the
+// workspace traffic of s > 1 in the same unit — each split writes an M x TN partial tile (kTM / kKC = 8
+// chunks' worth of operand reads) and the reduce reads s of them and writes one, at 1.5x a chunk's
+// cost per byte (profiles/grad_gemm_splits_r05.json: at cfg2 b8 this picks 1 and 2 splits where the
+// round-count-only rule picked 8 and 6, 1.12 vs 1.35 ms for the two GEMMs); a larger s must win by 3 %.
+// RMD_GG_MAXSPLIT caps s, RMD_GG_OLDPLAN=1 restores the round-4 rule (A/B builds).
+#ifndef RMD_GG_MAXSPLIT
+#define RMD_GG_MAXSPLIT 8
+#endif
+#ifndef RMD_GG_OLDPLAN
+#define RMD_GG_OLDPLAN 0
+#endif
 Plan plan(int batch, int M, int K, int Nc) {
     Plan pl{};
     pl.tn = tile_n(Nc);
@@ -311,11 +321,20 @@ Plan plan(int batch, int M, int K, int Nc) {
     const int nch = (K + kKC - 1) / kKC;
     double best = 1e30;
     pl.splits = 1;
-    for (int s = 1; s <= 8 && s <= nch; ++s) {
+    for (int s = 1; s <= RMD_GG_MAXSPLIT && s <= nch; ++s) {
         const long long rounds = (tiles * s + 255) / 256;
         const int per = (nch + s - 1) / s;
-        const double cost = (double)rounds * per + (s > 1 ? 0.15 * s * (double)tiles / 256.0 : 0.0);
-        if (cost < best - 1e-9) {
+        if (RMD_GG_OLDPLAN) {
+            const double cost = (double)rounds * per + (s > 1 ? 0.15 * s * (double)tiles / 256.0 : 0.0);
+            if (cost < best - 1e-9) {
+                best = cost;
+                pl.splits = s;
+            }
+            continue;
+        }
+        const double ws = s > 1 ? 1.5 * (kTM / kKC) * (2.0 * s + 1.0) * (double)tiles / 256.0 : 0.0;
+        const double cost = (double)rounds * per + ws;
+        if (cost < best * 0.97) {
             best = cost;
             pl.splits = s;
         }

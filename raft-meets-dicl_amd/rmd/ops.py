@@ -275,12 +275,18 @@ def otf_lookup_autograd(token, state, coords, radius, mask_costs=()):
 #
 # The pyramid Function returns a scalar "token" that every lookup of the same CorrBlock takes as an
 # input, so autograd runs all lookup backwards before the pyramid backward.  Each lookup backward
-# accumulates into ONE dense fp32 gradient G over the T' padded targets, in the pyramid's chunked
-# query-minor order (8-target chunks, include/rmd.h, rmd_corr_lookup_backward), shared through
-# _CorrState; the pyramid backward then turns G into d fmap1 / d fmap2 with two MFMA GEMMs that read G
-# in its blocked order (rmd_corr_grad_gemm layouts 3 / 2, no transpose pass; split-bf16 products in the
-# fp32 modes, bf16 products with fp32 accumulation in the bf16 modes) and the native pool / unpool
-# kernels (G, pool and unpool in fp32 in every mode).
+# only hands its grad_out and coordinates to the shared _CorrState; the pyramid backward writes ONE
+# dense fp32 gradient G over the T' padded targets, in the pyramid's chunked query-minor order
+# (8-target chunks, include/rmd.h), from all of them in one pass (rmd_corr_grad_build: the sums of
+# one rmd_corr_lookup_backward per lookup into a zeroed G, in the same order, without the zero fill
+# and the per-lookup read-modify-write passes), then turns G into d fmap1 / d fmap2 with two MFMA
+# GEMMs that read G in its blocked order (rmd_corr_grad_gemm layouts 3 / 2, no transpose pass;
+# split-bf16 products in the fp32 modes, bf16 products with fp32 accumulation in the bf16 modes) and
+# the native pool / unpool kernels (G, pool and unpool in fp32 in every mode).
+
+# False: one rmd_corr_lookup_backward per lookup into a zeroed G (the round-4 path; A/B only)
+GRAD_BUILD = True
+
 
 class _CorrState:
     def __init__(self, pyr, f1, f2, precision):
@@ -288,7 +294,8 @@ class _CorrState:
         self.f1 = f1
         self.f2 = f2
         self.precision = precision
-        self.grad = None          # dense G, allocated by the first lookup backward
+        self.grad = None          # dense G (GRAD_BUILD False: allocated by the first lookup backward)
+        self.pending = []         # (grad_out, coords, radius, level mask) per lookup backward, in order
 
 
 def _mask_bits(mask_costs, levels):
@@ -297,6 +304,31 @@ def _mask_bits(mask_costs, levels):
         if 0 <= m - 3 < levels:
             mask |= 1 << (m - 3)
     return mask
+
+
+def _build_grad(st):
+    """G from the pending lookup gradients (rmd_corr_grad_build), consecutive equal radii per launch."""
+    d = st.pyr.desc
+    lib = _lib.lib()
+    t = lib.rmd_corr_grad_targets(d.height, d.width, d.levels)
+    pend, st.pending = st.pending, []
+    dev = pend[0][0].device
+    G = torch.empty(d.batch * d.height * d.width * t, dtype=torch.float32, device=dev)
+    i = 0
+    with torch.cuda.device(dev):
+        stream = _stream(G)
+        while i < len(pend):
+            j = i
+            while j < len(pend) and pend[j][2] == pend[i][2]:
+                j += 1
+            grp = pend[i:j]
+            gouts = (ctypes.c_void_p * len(grp))(*[x[0].data_ptr() for x in grp])
+            cos = (ctypes.c_void_p * len(grp))(*[x[1].data_ptr() for x in grp])
+            masks = (ctypes.c_uint * len(grp))(*[x[3] for x in grp])
+            _lib.check(lib.rmd_corr_grad_build(gouts, cos, masks, len(grp), ctypes.byref(d), grp[0][2],
+                                               1 if i > 0 else 0, _ptr(G), stream), "rmd_corr_grad_build")
+            i = j
+    return G
 
 
 class _CorrPyramidFn(torch.autograd.Function):
@@ -314,6 +346,8 @@ class _CorrPyramidFn(torch.autograd.Function):
         b, c, h, w = f1.shape
         n = h * w
         levels = st.pyr.levels
+        if st.pending:
+            st.grad = _build_grad(st)
         if st.grad is None:
             return torch.zeros_like(f1), torch.zeros_like(f2), None
         lib = _lib.lib()
@@ -361,12 +395,16 @@ class _CorrLookupFn(torch.autograd.Function):
     def backward(ctx, gout):
         (co,) = ctx.saved_tensors
         st = ctx.state
+        g = gout.float().contiguous()
+        if GRAD_BUILD:
+            # G is written from every lookup's gradient at once by the pyramid backward
+            st.pending.append((g, co, ctx.radius, ctx.mask))
+            return gout.new_zeros(()), None, None, None, None
         d = st.pyr.desc
         lib = _lib.lib()
         if st.grad is None:
             t = lib.rmd_corr_grad_targets(d.height, d.width, d.levels)
             st.grad = torch.zeros(d.batch * d.height * d.width * t, dtype=torch.float32, device=co.device)
-        g = gout.float().contiguous()
         with torch.cuda.device(co.device):
             _lib.check(lib.rmd_corr_lookup_backward(_ptr(g), ctx_desc(st), _ptr(co), ctx.radius, ctx.mask,
                                                     _ptr(st.grad), _stream(co)), "rmd_corr_lookup_backward")

@@ -2,8 +2,9 @@
 """RAFT correlation forward + backward timing (training path, diagnostic; MI355X only).
 
 rmd.raft.CorrBlock with feature maps that require gradients: the pyramid (GEMM + pooled epilogue),
-12 lookups, then autograd: 12 rmd_corr_lookup_backward into the dense query-minor G, the pooled
-target features, two GEMMs and the unpool kernel.  Shape: FlyingChairs 368x496 -> 46x62 (RAFT pads
+12 lookups, then autograd: G of the 12 lookups written in one pass (rmd_corr_grad_build; with
+RMD_GRAD_BUILD=0 the round-4 path: 12 rmd_corr_lookup_backward into a zeroed G), the pooled target
+features, two GEMMs and the unpool kernel.  Shape: FlyingChairs 368x496 -> 46x62 (RAFT pads
 modulo 8), C = 256, batch 6 (SURVEY.md §8(d) cfg5 batch), smooth moving coordinates.
 usage: bench_corr_bwd.py [reps] [precision] [cfg5|cfg2]   -> one JSON document on stdout
 (cfg2: bench.py's headline shape, 55x128, batch 8)
@@ -23,6 +24,8 @@ import bench  # noqa: E402
 
 def main():
     import rmd
+    from rmd import ops
+    ops.GRAD_BUILD = os.environ.get("RMD_GRAD_BUILD", "1") != "0"
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     shape = sys.argv[3] if len(sys.argv) > 3 else "cfg5"
@@ -62,7 +65,8 @@ def main():
     # the same backward driven by the 12 upstream gradients directly (no torch loss multiply / sum /
     # their backward): the correlation block's own backward kernels
     t_fb2 = run(lambda: torch.autograd.grad(fwd_outs(), (f1, f2), gos), reps)
-    print(json.dumps({"shape": f"B{b} C{c} {h}x{w}, 12 lookups", "precision": prec, "forward_ms": t_f,
+    print(json.dumps({"shape": f"B{b} C{c} {h}x{w}, 12 lookups", "precision": prec,
+                      "grad_build": ops.GRAD_BUILD, "forward_ms": t_f,
                       "forward_backward_ms": t_fb, "backward_ms": t_fb - t_f,
                       "backward_ms_from_grad_out": t_fb2 - t_f,
                       "note": "backward_ms: forward_backward includes the loss multiply-adds (torch); "
