@@ -230,6 +230,14 @@ int rmd_corr_grad_build(const float* const* grad_outs, const float* const* coord
                         const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* desc, int radius,
                         int accumulate, float* grad_levels, void* stream);
 
+/* rmd_corr_grad_build with bf16_out != 0: G stored as bfloat16 (round to nearest even of the fp32 sums,
+ * the same element order, 2 bytes each) — what rmd_corr_grad_gemm_bf16g reads in the bf16 precision
+ * mode, whose fp32-G GEMM rounds G to bfloat16 on load anyway (bit-identical results, half the G
+ * traffic).  bf16_out requires accumulate == 0 and nlookups <= 16. */
+int rmd_corr_grad_build_ex(const float* const* grad_outs, const float* const* coords,
+                           const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* desc, int radius,
+                           int accumulate, int bf16_out, void* grad_levels, void* stream);
+
 /* pooled (B, C, T') = avg_pool_{2^l}(fmap2) * scale for every level, in G's padded target order (pad
  * targets 0) (raft.py:35-47 applied to the feature map, which commutes with the product). */
 int rmd_corr_pool_targets(const float* fmap2, int batch, int channels, int height, int width, int levels,
@@ -255,6 +263,13 @@ int rmd_corr_unpool_targets(const float* grad_pooled, int batch, int channels, i
 size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, int nc);
 int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m, int k, int nc,
                        int layout, int compute, float* out, void* workspace, void* stream);
+
+/* rmd_corr_grad_gemm with compute RMD_BF16 and a bfloat16 B (layouts 2 / 3: G from
+ * rmd_corr_grad_build_ex with bf16_out): the fp32-B GEMM rounds B to bfloat16 on load, so the result
+ * is bit-identical to rmd_corr_grad_gemm(..., RMD_BF16, ...) on the fp32 G; B's base 8-byte aligned
+ * for vector loads.  Same workspace as rmd_corr_grad_gemm_workspace_bytes. */
+int rmd_corr_grad_gemm_bf16g(const float* a, long long lda, const void* bm, long long ldb, int batch, int m, int k,
+                             int nc, int layout, float* out, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * DICL cost volumes.  Shapes: fmap1 (B, C, h, w); fmap2 (B, C, hl, wl); coords (B, 2, h, w);

@@ -238,9 +238,10 @@ struct BuildArgs {
 // the sequential kernel's +-1e6 clamp differs only where neither adds anything)
 __device__ __forceinline__ float build_coord(float c, float inv) { return fminf(fmaxf(c * inv, -30000.f), 30000.f); }
 
-template <int R, bool ACC>
+template <int R, bool ACC, bool BF>
 __global__ void __launch_bounds__(kBuildThreads)
 corr_grad_build_kernel(BuildArgs a, GradGeom g, float* __restrict__ grad) {
+    static_assert(!(ACC && BF), "a bfloat16 G is written by one launch (no accumulation)");
     constexpr int D = 2 * R + 1, K = 2 * R + 2;
     constexpr int RB = kBuildRows, CB = kBuildChunks, TS = kBuildSlots, TILE = RB * TS * kBuildThreads;
     __shared__ float tile[TILE];                             // [row][slot][query]
@@ -385,31 +386,57 @@ corr_grad_build_kernel(BuildArgs a, GradGeom g, float* __restrict__ grad) {
         {
             // per (row, chunk) the 64 queries' 32-B pieces are 2 KB contiguous; lane l stores the 16 B at
             // byte 16 l of each 1-KB half (query 32 h + l / 2, slots 4 (l & 1) ..), so every store
-            // instruction writes 8 whole 128-B lines; the tile is cleared for the next one on the way
-            float* __restrict__ gb = grad + (((size_t)b * g.TC + g.coff[L]) * N + p0) * kGcw +
-                                     ((size_t)y0 * nch + clo) * chs;
-            const int e0 = 4 * (lane & 1);
+            // instruction writes 8 whole 128-B lines; the tile is cleared for the next one on the way.
+            // BF: G in bfloat16 (round to nearest even of the fp32 sums): a piece is 16 B, lane l stores
+            // query l's (1 KB contiguous per row and chunk)
+            typedef __attribute__((ext_vector_type(4))) float f32x4;
 #pragma unroll
             for (int r = 0; r < RB; ++r)
 #pragma unroll
                 for (int k = 0; k < CB; ++k) {
                     if (r >= nr || k >= ncol) continue;
                     const int lim = lw - 8 * (clo + k);     // slots e < lim are on the level (pads stay 0)
+                    const size_t piece = (((size_t)b * g.TC + g.coff[L] + (size_t)(y0 + r) * nch + clo + k) * N + p0);
+                    if constexpr (BF) {
+                        float v[8];
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int q = 32 * h + (lane >> 1);
-                        float v[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            float* at = tb + (r * TS + 1 + 8 * k + e0 + j) * kBuildThreads + q;
-                            v[j] = e0 + j < lim ? *at : 0.f;
+                        for (int e = 0; e < 8; ++e) {
+                            float* at = tb + (r * TS + 1 + 8 * k + e) * kBuildThreads + lane;
+                            v[e] = e < lim ? *at : 0.f;
                             *at = 0.f;
                         }
-                        if (p0 + q < N) {
-                            typedef __attribute__((ext_vector_type(4))) float f32x4;
-                            f32x4* d = reinterpret_cast<f32x4*>(gb + ((size_t)r * nch + k) * chs + (size_t)q * kGcw + e0);
-                            if constexpr (RMD_BUILD_NT) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, d);
-                            else *d = f32x4{v[0], v[1], v[2], v[3]};
+                        if (p0 + lane < N) {
+                            unsigned w[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const __bf16 lo = (__bf16)v[2 * e], hi = (__bf16)v[2 * e + 1];
+                                w[e] = (unsigned)__builtin_bit_cast(unsigned short, lo) |
+                                       ((unsigned)__builtin_bit_cast(unsigned short, hi) << 16);
+                            }
+                            f32x4* d = reinterpret_cast<f32x4*>(reinterpret_cast<unsigned short*>(grad) +
+                                                                (piece + lane) * kGcw);
+                            const f32x4 o{__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                          __uint_as_float(w[3])};
+                            if constexpr (RMD_BUILD_NT) __builtin_nontemporal_store(o, d);
+                            else *d = o;
+                        }
+                    } else {
+                        const int e0 = 4 * (lane & 1);
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int q = 32 * h + (lane >> 1);
+                            float v[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                float* at = tb + (r * TS + 1 + 8 * k + e0 + j) * kBuildThreads + q;
+                                v[j] = e0 + j < lim ? *at : 0.f;
+                                *at = 0.f;
+                            }
+                            if (p0 + q < N) {
+                                f32x4* d = reinterpret_cast<f32x4*>(grad + (piece + q) * kGcw + e0);
+                                if constexpr (RMD_BUILD_NT) __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, d);
+                                else *d = f32x4{v[0], v[1], v[2], v[3]};
+                            }
                         }
                     }
                 }
@@ -511,6 +538,15 @@ extern "C" int rmd_corr_lookup_backward(const float* grad_out, const rmd_pyramid
 extern "C" int rmd_corr_grad_build(const float* const* grad_outs, const float* const* coords,
                                    const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* d,
                                    int radius, int accumulate, float* grad_levels, void* stream) {
+    return rmd_corr_grad_build_ex(grad_outs, coords, zero_level_masks, nlookups, d, radius, accumulate, 0, grad_levels,
+                                  stream);
+}
+
+extern "C" int rmd_corr_grad_build_ex(const float* const* grad_outs, const float* const* coords,
+                                      const unsigned* zero_level_masks, int nlookups, const rmd_pyramid_desc* d,
+                                      int radius, int accumulate, int bf16_out, void* grad_levels, void* stream) {
+    RMD_REQUIRE(!bf16_out || (!accumulate && nlookups <= rmd::kBuildMax), RMD_ERR_ARG,
+                "rmd_corr_grad_build: a bfloat16 G takes at most %d lookups and no accumulation", rmd::kBuildMax);
     RMD_REQUIRE(d && grad_levels && nlookups >= 0 && (nlookups == 0 || (grad_outs && coords)), RMD_ERR_ARG,
                 "rmd_corr_grad_build: null pointer or negative lookup count");
     RMD_REQUIRE(radius >= 1 && radius <= 8, RMD_ERR_SHAPE, "rmd_corr_grad_build: radius %d not in 1..8", radius);
@@ -538,6 +574,7 @@ extern "C" int rmd_corr_grad_build(const float* const* grad_outs, const float* c
                 units, d->batch);
     const dim3 grid((N + rmd::kBuildThreads - 1) / rmd::kBuildThreads, d->batch, units);
     hipStream_t st = rmd::as_stream(stream);
+    float* gl = static_cast<float*>(grad_levels);
     // one launch per kBuildMax lookups; after the first, each launch adds to G in lookup order
     for (int i0 = 0; i0 < nlookups || (i0 == 0 && !accumulate); i0 += rmd::kBuildMax) {
         a.n = nlookups - i0 < rmd::kBuildMax ? nlookups - i0 : rmd::kBuildMax;
@@ -550,8 +587,9 @@ extern "C" int rmd_corr_grad_build(const float* const* grad_outs, const float* c
         switch (radius) {
 #define RMD_CASE(RR)                                                                                              \
     case RR:                                                                                                      \
-        if (acc) rmd::corr_grad_build_kernel<RR, true><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, grad_levels);   \
-        else rmd::corr_grad_build_kernel<RR, false><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, grad_levels);     \
+        if (acc) rmd::corr_grad_build_kernel<RR, true, false><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, gl);      \
+        else if (bf16_out) rmd::corr_grad_build_kernel<RR, false, true><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, gl); \
+        else rmd::corr_grad_build_kernel<RR, false, false><<<grid, rmd::kBuildThreads, 0, st>>>(a, g, gl);        \
         break;
             RMD_CASE(1) RMD_CASE(2) RMD_CASE(3) RMD_CASE(4) RMD_CASE(5) RMD_CASE(6) RMD_CASE(7) RMD_CASE(8)
 #undef RMD_CASE

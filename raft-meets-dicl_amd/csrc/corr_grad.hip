@@ -43,6 +43,7 @@ template <int TN> constexpr int lds_buf() { return kLdsA + TN * kRowB; }
 struct GemmArgs {
     const float* A;
     const float* Bm;
+    const unsigned short* Bh;   // BBF: B as bfloat16 bits (layouts 2 / 3), instead of Bm
     float* out;                 // final output (splits == 1) or the split workspace
     long long lda, ldb;         // row strides (elements)
     long long sa, sb, so;       // batch strides (elements) of A, Bm, out
@@ -85,9 +86,13 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ at, int k, int
 // of the next chunk runs beside the current chunk's MFMAs (waves 0-3 and 4-7 share each SIMD).
 // X3 = false (compute RMD_BF16, the bf16 precision mode): one bf16 product per k-step (hi.hi), the lo
 // halves are neither split nor stored
-template <bool VA, bool VB, int LAYOUT, bool X3 = true, int TN = 128>
+// BBF (bf16 compute, layouts 2 / 3): B is bfloat16 already (rmd_corr_grad_build_ex's G): 8-byte loads of
+// 4 elements, stored to LDS as the hi operand without conversion — the same bits the fp32 path's
+// (__bf16) rounding produces from the fp32 G, at half the bytes
+template <bool VA, bool VB, int LAYOUT, bool X3 = true, int TN = 128, bool BBF = false>
 __global__ void __launch_bounds__(512, 1)
 grad_gemm_x3(GemmArgs p) {
+    static_assert(!BBF || (!X3 && LAYOUT >= 2), "bfloat16 B: bf16 compute, blocked layouts");
     constexpr int kTN = TN, kLdsBuf = lds_buf<TN>();
     constexpr int NJ = TN / 64;                 // 32-column MFMA tiles per wave (a wave owns 64 x TN/2)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -105,7 +110,8 @@ grad_gemm_x3(GemmArgs p) {
     const int m0 = tm * kTM, n0 = tn * kTN;
     const int kb = split * p.kper, ke = min(p.K, kb + p.kper);
     const float* __restrict__ A = p.A + (size_t)b * p.sa;
-    const float* __restrict__ Bm = p.Bm + (size_t)b * p.sb;
+    const float* __restrict__ Bm = BBF ? nullptr : p.Bm + (size_t)b * p.sb;
+    const unsigned short* __restrict__ Bh = BBF ? p.Bh + (size_t)b * p.sb : nullptr;
 
     // per thread: A 4 x float4 (rows m0 + 64 it + tid / 8, k 4 (tid % 8) .. +3); B TN / 64 x float4
     float4 ra[4], rb[TN / 64];
@@ -128,7 +134,19 @@ grad_gemm_x3(GemmArgs p) {
                     const int k = k0 + 2 * kq + r;
                     float4& d = rb[2 * nn + r];
                     d = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (k < ke) {
+                    if (BBF && k < ke) {
+                        const unsigned short* src = Bh + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
+                        uint2 v;
+                        if (VB && n + 3 < p.Nc) {
+                            v = *reinterpret_cast<const uint2*>(src);
+                        } else {
+                            const unsigned e0 = n + 0 < p.Nc ? src[0] : 0u, e1 = n + 1 < p.Nc ? src[1] : 0u;
+                            const unsigned e2 = n + 2 < p.Nc ? src[2] : 0u, e3 = n + 3 < p.Nc ? src[3] : 0u;
+                            v = make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
+                        }
+                        d.x = __uint_as_float(v.x);
+                        d.y = __uint_as_float(v.y);
+                    } else if (k < ke) {
                         const float* src = LAYOUT == 0 ? Bm + (size_t)k * p.ldb + n
                                                        : Bm + ((size_t)(n >> 3) * p.ldb + k) * 8 + (n & 7);
                         if (VB && n + 3 < p.Nc) {
@@ -147,6 +165,21 @@ grad_gemm_x3(GemmArgs p) {
             for (int it = 0; it < TN / 64; ++it) {
                 const int row = n0 + it * 64 + (tid >> 3), k = k0 + (tid & 7) * 4;
                 // layout 3: k .. k + 3 lie in one 8-block (k % 4 == 0), contiguous like layout 1's row
+                if constexpr (BBF) {
+                    const unsigned short* src = Bh + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7);
+                    uint2 v = make_uint2(0u, 0u);
+                    if (row < p.Nc) {
+                        if (VB && k + 3 < ke) {
+                            v = *reinterpret_cast<const uint2*>(src);
+                        } else {
+                            const unsigned e0 = k + 0 < ke ? src[0] : 0u, e1 = k + 1 < ke ? src[1] : 0u;
+                            const unsigned e2 = k + 2 < ke ? src[2] : 0u, e3 = k + 3 < ke ? src[3] : 0u;
+                            v = make_uint2(e0 | (e1 << 16), e2 | (e3 << 16));
+                        }
+                    }
+                    rb[it] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), 0.f, 0.f);
+                    continue;
+                }
                 const float* src = LAYOUT == 1 ? Bm + (size_t)row * p.ldb + k
                                                : Bm + ((size_t)(k >> 3) * p.ldb + row) * 8 + (k & 7);
                 rb[it] = row < p.Nc ? load4<VB>(src, k, ke) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -171,6 +204,16 @@ grad_gemm_x3(GemmArgs p) {
             for (int nn = 0; nn < TN / 128; ++nn) {
                 const int nr = (TN / 2) * (w >> 2) + 64 * nn + 4 * (lane >> 2);
                 const float4 r0 = rb[2 * nn], r1 = rb[2 * nn + 1];
+                if constexpr (BBF) {
+                    // 4 bf16 per k row packed in (x, y): column j is half j & 1 of word j >> 1
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const unsigned w0 = __float_as_uint(j < 2 ? r0.x : r0.y), w1 = __float_as_uint(j < 2 ? r1.x : r1.y);
+                        const unsigned h0 = (w0 >> (16 * (j & 1))) & 0xffffu, h1 = (w1 >> (16 * (j & 1))) & 0xffffu;
+                        *reinterpret_cast<unsigned*>(sB + (nr + j) * kRowB + kq * 4) = h0 | (h1 << 16);
+                    }
+                    continue;
+                }
                 const float c0[2] = {r0.x, r1.x}, c1[2] = {r0.y, r1.y};
                 const float c2[2] = {r0.z, r1.z}, c3[2] = {r0.w, r1.w};
                 const float* cols[4] = {c0, c1, c2, c3};
@@ -187,6 +230,11 @@ grad_gemm_x3(GemmArgs p) {
         } else {
 #pragma unroll
             for (int it = 0; it < TN / 64; ++it) {
+                if constexpr (BBF) {
+                    unsigned char* d = sB + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
+                    *reinterpret_cast<uint2*>(d) = make_uint2(__float_as_uint(rb[it].x), __float_as_uint(rb[it].y));
+                    continue;
+                }
                 bf16x4 hi, lo;
                 split4(rb[it].x, rb[it].y, rb[it].z, rb[it].w, hi, lo);
                 unsigned char* d = sB + (it * 64 + (tid >> 3)) * kRowB + (tid & 7) * 8;
@@ -348,6 +396,9 @@ Plan plan(int batch, int M, int K, int Nc) {
 template <bool VA, bool VB, int LAYOUT, int TN>
 void launch_gemm_tn(const GemmArgs& a, int nwg, bool x3, hipStream_t st) {
     auto k = x3 ? grad_gemm_x3<VA, VB, LAYOUT, true, TN> : grad_gemm_x3<VA, VB, LAYOUT, false, TN>;
+    if constexpr (LAYOUT >= 2) {
+        if (a.Bh) k = grad_gemm_x3<VA, VB, LAYOUT, false, TN, true>;
+    }
     // the >64 KB LDS opt-in is per device: set it before every launch (cheap host call), so a process
     // that launches on a second GPU gets it too
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -370,23 +421,27 @@ extern "C" size_t rmd_corr_grad_gemm_workspace_bytes(int batch, int m, int k, in
     return pl.splits > 1 ? (size_t)pl.splits * batch * m * nc * sizeof(float) : 0;
 }
 
-extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m,
-                                  int k, int nc, int layout, int compute, float* out, void* workspace, void* stream) {
-    RMD_REQUIRE(a && bm && out, RMD_ERR_ARG, "rmd_corr_grad_gemm: null pointer");
+namespace rmd {
+namespace {
+int grad_gemm_impl(const float* a, long long lda, const float* bm, const unsigned short* bh, long long ldb, int batch,
+                   int m, int k, int nc, int layout, int compute, float* out, void* workspace, void* stream) {
+    RMD_REQUIRE(a && (bm || bh) && out, RMD_ERR_ARG, "rmd_corr_grad_gemm: null pointer");
     RMD_REQUIRE(compute == RMD_BF16X3 || compute == RMD_BF16, RMD_ERR_ARG,
                 "rmd_corr_grad_gemm: compute must be RMD_BF16X3 or RMD_BF16");
     const bool x3 = compute == RMD_BF16X3;
     RMD_REQUIRE(batch > 0 && m > 0 && k > 0 && nc > 0, RMD_ERR_SHAPE, "rmd_corr_grad_gemm: empty shape");
     RMD_REQUIRE(layout >= 0 && layout <= 3, RMD_ERR_ARG, "rmd_corr_grad_gemm: layout must be 0..3");
+    RMD_REQUIRE(!bh || (layout >= 2 && !x3), RMD_ERR_ARG, "rmd_corr_grad_gemm_bf16g: layouts 2 / 3 only");
     RMD_REQUIRE(lda >= k && ldb >= (layout == 0 ? nc : layout == 3 ? nc : k), RMD_ERR_SHAPE,
                 "rmd_corr_grad_gemm: bad row stride");
-    const rmd::Plan pl = rmd::plan(batch, m, k, nc);
+    const Plan pl = plan(batch, m, k, nc);
     RMD_REQUIRE(pl.splits == 1 || workspace, RMD_ERR_ARG, "rmd_corr_grad_gemm: workspace required (%d splits)",
                 pl.splits);
-    hipStream_t st = rmd::as_stream(stream);
-    rmd::GemmArgs g{};
+    hipStream_t st = as_stream(stream);
+    GemmArgs g{};
     g.A = a;
     g.Bm = bm;
+    g.Bh = bh;
     g.out = pl.splits > 1 ? static_cast<float*>(workspace) : out;
     g.lda = lda;
     g.ldb = ldb;
@@ -409,25 +464,40 @@ extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm
     RMD_REQUIRE(nwg < (1LL << 31), RMD_ERR_SHAPE, "rmd_corr_grad_gemm: grid too large");
     // float4 paths need 16-B aligned rows: row stride % 4 == 0 AND a 16-B aligned base pointer (a
     // caller may pass an offset view); layouts 2 / 3 need only the base (4 consecutive elements of an
-    // 8-block are contiguous)
-    const bool a16 = ((uintptr_t)a & 15) == 0, b16 = ((uintptr_t)bm & 15) == 0;
+    // 8-block are contiguous; 8-B aligned for a bfloat16 B)
+    const bool a16 = ((uintptr_t)a & 15) == 0;
+    const bool b16 = bh ? ((uintptr_t)bh & 7) == 0 : ((uintptr_t)bm & 15) == 0;
     const bool va = a16 && (lda & 3) == 0;
     bool vb = b16 && (ldb & 3) == 0;
 #define RMD_GG(VA, VB)                                                                      \
-    (layout == 0 ? rmd::launch_gemm<VA, VB, 0>(g, (int)nwg, x3, pl.tn, st)                  \
-     : layout == 1 ? rmd::launch_gemm<VA, VB, 1>(g, (int)nwg, x3, pl.tn, st)                \
-     : layout == 2 ? rmd::launch_gemm<VA, VB, 2>(g, (int)nwg, x3, pl.tn, st)                \
-                   : rmd::launch_gemm<VA, VB, 3>(g, (int)nwg, x3, pl.tn, st))
-    if (layout >= 2) vb = b16;                 // 8-blocks: 4 consecutive elements are contiguous, 16-B aligned
+    (layout == 0 ? launch_gemm<VA, VB, 0>(g, (int)nwg, x3, pl.tn, st)                       \
+     : layout == 1 ? launch_gemm<VA, VB, 1>(g, (int)nwg, x3, pl.tn, st)                     \
+     : layout == 2 ? launch_gemm<VA, VB, 2>(g, (int)nwg, x3, pl.tn, st)                     \
+                   : launch_gemm<VA, VB, 3>(g, (int)nwg, x3, pl.tn, st))
+    if (layout >= 2) vb = b16;                 // 8-blocks: 4 consecutive elements are contiguous, aligned
     if (va && vb) RMD_GG(true, true);
     else if (va) RMD_GG(true, false);
     else if (vb) RMD_GG(false, true);
     else RMD_GG(false, false);
 #undef RMD_GG
-    int rc = rmd::check_launch("rmd_corr_grad_gemm");
+    int rc = check_launch("rmd_corr_grad_gemm");
     if (rc != RMD_OK || pl.splits == 1) return rc;
     const long long n = (long long)batch * m * nc;
     const long long blocks = (n / 4 + 255) / 256 + 1;
-    rmd::grad_gemm_reduce<<<(unsigned)blocks, 256, 0, st>>>(static_cast<const float*>(workspace), n, pl.splits, out);
-    return rmd::check_launch("rmd_corr_grad_gemm reduce");
+    grad_gemm_reduce<<<(unsigned)blocks, 256, 0, st>>>(static_cast<const float*>(workspace), n, pl.splits, out);
+    return check_launch("rmd_corr_grad_gemm reduce");
+}
+}  // namespace
+}  // namespace rmd
+
+extern "C" int rmd_corr_grad_gemm(const float* a, long long lda, const float* bm, long long ldb, int batch, int m,
+                                  int k, int nc, int layout, int compute, float* out, void* workspace, void* stream) {
+    return rmd::grad_gemm_impl(a, lda, bm, nullptr, ldb, batch, m, k, nc, layout, compute, out, workspace, stream);
+}
+
+extern "C" int rmd_corr_grad_gemm_bf16g(const float* a, long long lda, const void* bm, long long ldb, int batch, int m,
+                                        int k, int nc, int layout, float* out, void* workspace, void* stream) {
+    RMD_REQUIRE(bm, RMD_ERR_ARG, "rmd_corr_grad_gemm_bf16g: null pointer");
+    return rmd::grad_gemm_impl(a, lda, nullptr, static_cast<const unsigned short*>(bm), ldb, batch, m, k, nc, layout,
+                               RMD_BF16, out, workspace, stream);
 }

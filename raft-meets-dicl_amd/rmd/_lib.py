@@ -65,6 +65,9 @@ _SIGS = {
     "rmd_corr_lookup_backward": (_I, [_P, ctypes.POINTER(PyramidDesc), _P, _I, _U, _P, _P]),
     "rmd_corr_grad_build": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_U), _I,
                                  ctypes.POINTER(PyramidDesc), _I, _I, _P, _P]),
+    "rmd_corr_grad_build_ex": (_I, [ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_U), _I,
+                                    ctypes.POINTER(PyramidDesc), _I, _I, _I, _P, _P]),
+    "rmd_corr_grad_gemm_bf16g": (_I, [_P, ctypes.c_longlong, _P, ctypes.c_longlong, _I, _I, _I, _I, _I, _P, _P, _P]),
     "rmd_corr_pool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_corr_unpool_targets": (_I, [_P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_corr_grad_gemm_workspace_bytes": (ctypes.c_size_t, [_I, _I, _I, _I]),

@@ -286,6 +286,9 @@ def otf_lookup_autograd(token, state, coords, radius, mask_costs=()):
 
 # False: one rmd_corr_lookup_backward per lookup into a zeroed G (the round-4 path; A/B only)
 GRAD_BUILD = True
+# bf16 modes: G written as bfloat16 by the build and read by the bf16-B grad GEMMs (bit-identical to
+# the fp32 G, whose GEMM rounds it to bfloat16 on load; half the G traffic).  False: fp32 G (A/B only)
+GRAD_BF16 = True
 
 
 class _CorrState:
@@ -306,14 +309,15 @@ def _mask_bits(mask_costs, levels):
     return mask
 
 
-def _build_grad(st):
-    """G from the pending lookup gradients (rmd_corr_grad_build), consecutive equal radii per launch."""
+def _build_grad(st, bf16=False):
+    """G from the pending lookup gradients (rmd_corr_grad_build), consecutive equal radii per launch;
+    bf16: one launch writes a bfloat16 G (the caller checked one radius, <= 16 lookups)."""
     d = st.pyr.desc
     lib = _lib.lib()
     t = lib.rmd_corr_grad_targets(d.height, d.width, d.levels)
     pend, st.pending = st.pending, []
     dev = pend[0][0].device
-    G = torch.empty(d.batch * d.height * d.width * t, dtype=torch.float32, device=dev)
+    G = torch.empty(d.batch * d.height * d.width * t, dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
     i = 0
     with torch.cuda.device(dev):
         stream = _stream(G)
@@ -325,8 +329,9 @@ def _build_grad(st):
             gouts = (ctypes.c_void_p * len(grp))(*[x[0].data_ptr() for x in grp])
             cos = (ctypes.c_void_p * len(grp))(*[x[1].data_ptr() for x in grp])
             masks = (ctypes.c_uint * len(grp))(*[x[3] for x in grp])
-            _lib.check(lib.rmd_corr_grad_build(gouts, cos, masks, len(grp), ctypes.byref(d), grp[0][2],
-                                               1 if i > 0 else 0, _ptr(G), stream), "rmd_corr_grad_build")
+            _lib.check(lib.rmd_corr_grad_build_ex(gouts, cos, masks, len(grp), ctypes.byref(d), grp[0][2],
+                                                  1 if i > 0 else 0, 1 if bf16 else 0, _ptr(G), stream),
+                       "rmd_corr_grad_build")
             i = j
     return G
 
@@ -346,8 +351,10 @@ class _CorrPyramidFn(torch.autograd.Function):
         b, c, h, w = f1.shape
         n = h * w
         levels = st.pyr.levels
+        bf16_mode = PRECISIONS[st.precision][0] == RMD_BF16
         if st.pending:
-            st.grad = _build_grad(st)
+            one_launch = len(st.pending) <= 16 and len({x[2] for x in st.pending}) == 1
+            st.grad = _build_grad(st, bf16=GRAD_BF16 and bf16_mode and one_launch)
         if st.grad is None:
             return torch.zeros_like(f1), torch.zeros_like(f2), None
         lib = _lib.lib()
@@ -368,11 +375,18 @@ class _CorrPyramidFn(torch.autograd.Function):
             # grad_fmap1 = P G (K = T', layout 3: G blocked along k), dP = fmap1 G^T (K = N, layout 2: G
             # blocked along n): MFMA GEMMs (corr_grad.hip) in the block's compute — split-bf16 (fp32
             # accuracy) for the fp32 modes, one bf16 product for the bf16 modes
-            gc = RMD_BF16 if PRECISIONS[st.precision][0] == RMD_BF16 else RMD_BF16X3
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, gc, _ptr(g1), _ptr(ws),
-                                              stream), "rmd_corr_grad_gemm")
-            _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, gc, _ptr(dpool), _ptr(ws),
-                                              stream), "rmd_corr_grad_gemm")
+            gc = RMD_BF16 if bf16_mode else RMD_BF16X3
+            if G.dtype == torch.bfloat16:
+                # bfloat16 G (bf16 modes): the same products as the fp32-G GEMM, half the bytes
+                _lib.check(lib.rmd_corr_grad_gemm_bf16g(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, _ptr(g1),
+                                                        _ptr(ws), stream), "rmd_corr_grad_gemm_bf16g")
+                _lib.check(lib.rmd_corr_grad_gemm_bf16g(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, _ptr(dpool),
+                                                        _ptr(ws), stream), "rmd_corr_grad_gemm_bf16g")
+            else:
+                _lib.check(lib.rmd_corr_grad_gemm(_ptr(pooled), t, _ptr(G), n, b, c, t, n, 3, gc, _ptr(g1),
+                                                  _ptr(ws), stream), "rmd_corr_grad_gemm")
+                _lib.check(lib.rmd_corr_grad_gemm(_ptr(f1), n, _ptr(G), n, b, c, n, t, 2, gc, _ptr(dpool),
+                                                  _ptr(ws), stream), "rmd_corr_grad_gemm")
             _lib.check(lib.rmd_corr_unpool_targets(_ptr(dpool), b, c, h, w, levels, scale, _ptr(g2), stream),
                        "rmd_corr_unpool_targets")
         st.grad = None

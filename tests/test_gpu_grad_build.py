@@ -147,3 +147,88 @@ def test_autograd_path_uses_build_and_matches_sequential_path():
     a1, a2 = grads(True)
     s1, s2 = grads(False)
     assert torch.equal(a1, s1) and torch.equal(a2, s2)
+
+
+def _build_bf16(d, lookups, radius, masks):
+    L = _lib()
+    t = L.lib().rmd_corr_grad_targets(d.height, d.width, d.levels)
+    G = torch.full((d.batch * d.height * d.width * t,), float("nan"), dtype=torch.bfloat16, device="cuda")
+    n = len(lookups)
+    gouts = (ctypes.c_void_p * max(n, 1))(*[go.data_ptr() for go, _ in lookups])
+    cos = (ctypes.c_void_p * max(n, 1))(*[co.data_ptr() for _, co in lookups])
+    ms = (ctypes.c_uint * max(n, 1))(*masks)
+    L.check(L.lib().rmd_corr_grad_build_ex(gouts, cos, ms, n, ctypes.byref(d), radius, 0, 1,
+                                           ctypes.c_void_p(G.data_ptr()), None), "grad_build_ex")
+    return G
+
+
+@pytest.mark.parametrize("b,h,w,levels,radius,n", [(2, 19, 26, 4, 3, 3), (1, 55, 128, 4, 4, 12), (3, 9, 70, 4, 4, 5)])
+def test_bf16_build_is_the_rounded_fp32_build(b, h, w, levels, radius, n):
+    """bf16_out: every element is the round-to-nearest-even bfloat16 of the fp32 build's sum."""
+    d = _desc(b, h, w, levels)
+    lk = _inputs(b, h, w, levels, radius, n, seed=7 + n)
+    masks = [0] * n
+    g32 = _build(d, lk, radius, masks)
+    g16 = _build_bf16(d, lk, radius, masks)
+    assert torch.equal(g16.view(torch.int16), g32.to(torch.bfloat16).view(torch.int16))
+
+
+def test_bf16_build_rejects_accumulation_and_long_lists():
+    L = _lib()
+    d = _desc(1, 9, 12, 2)
+    G = torch.empty(10, dtype=torch.bfloat16, device="cuda")
+    assert L.lib().rmd_corr_grad_build_ex(None, None, None, 0, ctypes.byref(d), 4, 1, 1,
+                                          ctypes.c_void_p(G.data_ptr()), None) == -1
+    p = (ctypes.c_void_p * 17)(*([G.data_ptr()] * 17))
+    assert L.lib().rmd_corr_grad_build_ex(p, p, None, 17, ctypes.byref(d), 4, 0, 1,
+                                          ctypes.c_void_p(G.data_ptr()), None) == -1
+
+
+@pytest.mark.parametrize("layout", [2, 3])
+@pytest.mark.parametrize("b,m,k,nc", [(2, 256, 3896, 2852), (1, 100, 37, 45), (3, 256, 1000, 9), (1, 48, 8, 1030)])
+def test_bf16g_gemm_equals_fp32g_gemm_in_bf16_compute(layout, b, m, k, nc):
+    """rmd_corr_grad_gemm_bf16g on the bfloat16 B == rmd_corr_grad_gemm(RMD_BF16) on the fp32 B, bitwise."""
+    L = _lib()
+    lib = L.lib()
+    rng = np.random.default_rng(b * 1000 + k)
+    a = torch.tensor(rng.standard_normal((b, m, k)), dtype=torch.float32, device="cuda")
+    # B in the blocked layout: 2 = ((n/8) ldb + k) 8 + n%8 (ldb = k), 3 = ((k/8) ldb + n) 8 + k%8 (ldb = nc)
+    blocks = (nc + 7) // 8 if layout == 2 else (k + 7) // 8
+    ldb = k if layout == 2 else nc
+    bm = torch.tensor(rng.standard_normal((b, blocks * ldb * 8)), dtype=torch.float32, device="cuda")
+    bh = bm.to(torch.bfloat16)
+    ws = torch.empty(max(lib.rmd_corr_grad_gemm_workspace_bytes(b, m, k, nc), 1), dtype=torch.uint8, device="cuda")
+    o32 = torch.empty((b, m, nc), dtype=torch.float32, device="cuda")
+    o16 = torch.empty_like(o32)
+    P = ctypes.c_void_p
+    L.check(lib.rmd_corr_grad_gemm(P(a.data_ptr()), k, P(bm.data_ptr()), ldb, b, m, k, nc, layout, L.RMD_BF16,
+                                   P(o32.data_ptr()), P(ws.data_ptr()), None), "gemm")
+    L.check(lib.rmd_corr_grad_gemm_bf16g(P(a.data_ptr()), k, P(bh.data_ptr()), ldb, b, m, k, nc, layout,
+                                         P(o16.data_ptr()), P(ws.data_ptr()), None), "gemm_bf16g")
+    assert torch.equal(o16, o32)
+
+
+def test_autograd_bf16_mode_bf16_g_matches_fp32_g():
+    """bf16 precision: the bfloat16-G backward (product) and the fp32-G backward give identical grads."""
+    import rmd
+    from rmd import ops
+    rng = np.random.default_rng(12)
+    b, c, h, w = 2, 64, 23, 40
+    f1 = torch.tensor(rng.standard_normal((b, c, h, w)), dtype=torch.float32, device="cuda")
+    f2 = torch.tensor(rng.standard_normal((b, c, h, w)), dtype=torch.float32, device="cuda")
+    lk = _inputs(b, h, w, 4, 4, 6, seed=4)
+
+    def grads(flag):
+        ops.GRAD_BF16 = flag
+        try:
+            t1, t2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+            cb = rmd.raft.CorrBlock(t1, t2, 4, 4, precision="bf16")
+            loss = sum((cb(co) * go).sum() for go, co in lk)
+            loss.backward()
+            return t1.grad, t2.grad
+        finally:
+            ops.GRAD_BF16 = True
+
+    a1, a2 = grads(True)
+    s1, s2 = grads(False)
+    assert torch.isfinite(a1).all() and torch.equal(a1, s1) and torch.equal(a2, s2)

@@ -26,6 +26,7 @@ def main():
     import rmd
     from rmd import ops
     ops.GRAD_BUILD = os.environ.get("RMD_GRAD_BUILD", "1") != "0"
+    ops.GRAD_BF16 = os.environ.get("RMD_GRAD_BF16", "1") != "0"
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     prec = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     shape = sys.argv[3] if len(sys.argv) > 3 else "cfg5"
@@ -66,7 +67,8 @@ def main():
     # their backward): the correlation block's own backward kernels
     t_fb2 = run(lambda: torch.autograd.grad(fwd_outs(), (f1, f2), gos), reps)
     print(json.dumps({"shape": f"B{b} C{c} {h}x{w}, 12 lookups", "precision": prec,
-                      "grad_build": ops.GRAD_BUILD, "forward_ms": t_f,
+                      "grad_build": ops.GRAD_BUILD, "grad_bf16": ops.GRAD_BF16,
+                      "forward_ms": t_f,
                       "forward_backward_ms": t_fb, "backward_ms": t_fb - t_f,
                       "backward_ms_from_grad_out": t_fb2 - t_f,
                       "note": "backward_ms: forward_backward includes the loss multiply-adds (torch); "
