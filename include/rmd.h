@@ -439,8 +439,15 @@ int rmd_input_flow(const float* flow, const unsigned char* valid, int batch, int
 /* Message for the last failing call on this thread ("" if none). */
 const char* rmd_last_error(void);
 
-/* Library version string, e.g. "rmd 0.1 gfx950". */
+/* Library version string, e.g. "rmd 0.2 gfx950 abi 2". */
 const char* rmd_version(void);
+
+/* ABI revision of the exported signatures.  A binding checks it against the RMD_ABI_VERSION of the
+ * header it was written for and refuses a mismatch (rmd/_lib.py does).  History:
+ *   1  rounds 1-4
+ *   2  rmd_corr_grad_gemm gained `compute` (RMD_BF16X3 / RMD_BF16) before `out` (round 5) */
+#define RMD_ABI_VERSION 2
+int rmd_abi_version(void);
 
 #ifdef __cplusplus
 }

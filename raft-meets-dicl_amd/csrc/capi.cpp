@@ -24,7 +24,9 @@ static int level_chunk(int l) { return l <= 1 ? 8 : (l == 2 ? 4 : 2); }
 
 extern "C" const char* rmd_last_error(void) { return rmd::g_err; }
 
-extern "C" const char* rmd_version(void) { return "rmd 0.1 gfx950"; }
+extern "C" const char* rmd_version(void) { return "rmd 0.2 gfx950 abi 2"; }
+
+extern "C" int rmd_abi_version(void) { return RMD_ABI_VERSION; }
 
 extern "C" int rmd_pyramid_describe_layout(int batch, int height, int width, int levels, int storage, int layout,
                                            rmd_pyramid_desc* d) {

@@ -796,11 +796,15 @@ struct BwdWmax {                // header words of up to kMaxRecAll records (the
 };
 
 // fixed-point exponent s: 2^s * bound <= 2^62 with bound = nrec * N * max|w| * max|q~| (a power of two
-// scale, the same for every workgroup: deterministic)
-__device__ __forceinline__ int fixed_exp(float bound) {
-    if (!(bound > 0.f) || !__builtin_isfinite(bound)) return 60;
+// scale, the same for every workgroup: deterministic).  The bound is formed in double: the maxima are
+// finite floats, so it stays finite (<= 2^64 * FLT_MAX^2) where a float product would overflow to inf
+// (ADVICE r05); a zero bound (no nonzero contribution) takes any exponent, and a non-finite one — not
+// reachable from finite maxima — the smallest, so no sum can overflow.
+__device__ __forceinline__ int fixed_exp(double bound) {
+    if (!__builtin_isfinite(bound)) return -960;
+    if (!(bound > 0.0)) return 60;
     int e;
-    (void)frexpf(bound, &e);                         // bound < 2^e
+    (void)frexp(bound, &e);                          // bound < 2^e
     return max(-960, min(960, 62 - e));
 }
 
@@ -1127,8 +1131,8 @@ __global__ void otf_fixed_exp_kernel(const unsigned* __restrict__ wmax, const un
     unsigned mq = qmax[threadIdx.x];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) mq = max(mq, (unsigned)__shfl_xor((int)mq, o));
-    const float bound = (float)nrec * (float)N * __uint_as_float(*wmax) * __uint_as_float(mq);
-    if (threadIdx.x == 0) *sexp = fixed_exp(bound * 1.0001f);
+    const double bound = (double)nrec * (double)N * (double)__uint_as_float(*wmax) * (double)__uint_as_float(mq);
+    if (threadIdx.x == 0) *sexp = fixed_exp(bound * 1.0001);
 }
 
 // d fmap2[b, c, y, x] = sum_l d P_l[b, (y >> l, x >> l), c] / 4^l over the floor-cropped part of each level

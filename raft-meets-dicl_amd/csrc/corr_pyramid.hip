@@ -719,6 +719,14 @@ struct EpiState {
 // Epilogue piece s (0..15) of one tile, from accumulator set `acc`: level-0 chunk row m = s/2 of
 // column group tc = s%2, the level-1 sums of those rows, and every 4th / 8th / 16th piece the level-1
 // / level-2 / level-3 stores — so the pieces can ride along the k-steps of the next tile.
+// A/B knob (tools/build_variant.sh; the product build uses the default): RMD_W8_AUXH = cache-policy
+// bits of the level 1-3 stores (-1: the same as level 0's AUX)
+#ifndef RMD_W8_AUXH
+#define RMD_W8_AUXH -1
+#endif
+template <int AUX>
+constexpr int kAuxUpper = RMD_W8_AUXH < 0 ? AUX : RMD_W8_AUXH;
+
 template <int S, int AUX>
 __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, const LaneOff& lo, EpiState& st) {
     constexpr int m = S >> 1, tc = S & 1;
@@ -750,7 +758,7 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         swp(x1, y1);
         const i32x4 d = {(int)x0, (int)y0, (int)x1, (int)y1};
         __builtin_amdgcn_raw_buffer_store_b128(d, c.l[1].rsrc,
-                                               (int)(lo.o1 + (unsigned)p * c.l[1].rs + (p >= 2 ? c.l[1].hd : 0u)), 0, AUX);
+                                               (int)(lo.o1 + (unsigned)p * c.l[1].rs + (p >= 2 ? c.l[1].hd : 0u)), 0, kAuxUpper<AUX>);
         // level-2 sums of level-2 row p: lane h holds cols {h, 2+h}
 #pragma unroll
         for (int cg = 0; cg < 2; ++cg)
@@ -764,7 +772,7 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         swp(x, y);          // lane h now holds row 2k+h: x = cols {0,2}, y = cols {1,3}
         const i32x2 d = {(int)__builtin_amdgcn_perm(y, x, 0x05040100u), (int)__builtin_amdgcn_perm(y, x, 0x07060302u)};
         __builtin_amdgcn_raw_buffer_store_b64(d, c.l[2].rsrc,
-                                              (int)(lo.o2 + (unsigned)(2 * k) * c.l[2].rs + (k >= 1 ? c.l[2].hd : 0u)), 0, AUX);
+                                              (int)(lo.o2 + (unsigned)(2 * k) * c.l[2].rs + (k >= 1 ? c.l[2].hd : 0u)), 0, kAuxUpper<AUX>);
     }
     if constexpr (S == 15) {
         // level 3: rows 0, 1 (level-2 rows 0-1 / 2-3), cols 0, 1 (level-2 cols {0,1} / {2,3});
@@ -782,7 +790,7 @@ __device__ __forceinline__ void epi_piece(const f32x16 (&acc)[8], const Ctx& c, 
         const float inv = 1.0f / 64.0f;
         const unsigned v = pk(inv * (__uint_as_float(x0) + __uint_as_float(y0)),
                               inv * (__uint_as_float(x1) + __uint_as_float(y1)));
-        __builtin_amdgcn_raw_buffer_store_b32((int)v, c.l[3].rsrc, (int)lo.o3, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b32((int)v, c.l[3].rsrc, (int)lo.o3, 0, kAuxUpper<AUX>);
     }
 }
 #undef V

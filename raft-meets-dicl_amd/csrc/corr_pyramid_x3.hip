@@ -165,10 +165,37 @@ __device__ __forceinline__ i32x3 pack24(float a, float b, float c, float d) {
                  (int)__builtin_amdgcn_perm(v3, v2, 0x07060503u)};
 }
 
+// RMD_S24 rounding of a value the x3 GEMM produces: u + 0x80, top 24 bits.  The general rule
+// (s24_round) keeps a NaN a NaN by OR-ing the quiet bit; here every NaN is an MFMA result from bf16
+// operands (payload = a bf16 NaN's, low 16 bits zero, quiet) or the default quiet NaN, passed through
+// v_add / v_mul of the pooling (which keep an input NaN's payload) — so the + 0x80 never carries out of
+// the low byte and u + 0x80 has the same top 24 bits as u | 0x00400000: one VALU op instead of five
+// (test_s24_pyramid_is_rounded_f32_pyramid checks a NaN query row bit for bit).
+__device__ __forceinline__ unsigned s24_gemm(float v) { return __float_as_uint(v) + 0x80u; }
+__device__ __forceinline__ i32x3 pack24g(unsigned a, unsigned b, unsigned c, unsigned d) {
+    const unsigned v0 = s24_gemm(__uint_as_float(a)), v1 = s24_gemm(__uint_as_float(b)),
+                   v2 = s24_gemm(__uint_as_float(c)), v3 = s24_gemm(__uint_as_float(d));
+    return i32x3{(int)__builtin_amdgcn_perm(v1, v0, 0x05030201u), (int)__builtin_amdgcn_perm(v2, v1, 0x06050302u),
+                 (int)__builtin_amdgcn_perm(v3, v2, 0x07060503u)};
+}
+
+// v_permlane16_swap: the odd 16-lane rows of x are exchanged with the even rows of y (x.row1 <-> y.row0,
+// x.row3 <-> y.row2)
+__device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
+    auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+}
+
 // A/B knob (tools/build_variant.sh -D...; the product build uses the default): RMD_X3_ABL = the
-// kernel's ablation (1 = drop every store through a zero descriptor range: timing only)
+// kernel's ablation (1 = drop every store through a zero descriptor range; 2 = no epilogue, the
+// phase barriers kept; 3 = no epilogue and no barriers: timing only)
 #ifndef RMD_X3_ABL
 #define RMD_X3_ABL 0
+#endif
+// RMD_X3_S24_R05 = 1: the round-5 S24 epilogue (epilogue16<true>) instead of epilogue16_s24 (A/B only)
+#ifndef RMD_X3_S24_R05
+#define RMD_X3_S24_R05 0
 #endif
 
 // ---- GEMM kernel (16x16x32 MFMA) ------------------------------------------------------------------
@@ -189,6 +216,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int kLds16 = 2 * 32 * 128 * 16;
 constexpr int kDR16 = 4;                     // B ring depth (k-steps of 32 channels; divides 8)
 constexpr int kEpiStores16 = 30;             // buffer stores of one epilogue16 (16 + 8 + 4 + 2)
+constexpr int kEpiStoresS24 = 23;            // buffer stores of one epilogue16_s24 (16 + 4 + 1 + 2)
 
 __device__ __forceinline__ int s16_row(int y, int x) { return (((y >> 1) * 2 + (x >> 3)) << 4) + ((y & 1) << 3) + (x & 7); }
 
@@ -327,6 +355,102 @@ __device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (
     }
 }
 
+// S24 epilogue (round 6).  The F32-style epilogue above spent ~875 VALU instructions per 32-query tile
+// (the NaN-safe rounding, per-store address arithmetic and ds_bpermute gathers) against the partner wave's
+// 384 MFMAs, whose issue gaps hold ~2 VALU each, so it stretched the MFMA phase and held the clock down
+// (profiles/x3_epi_r06.json).  This one computes the same values in the same order and stores the same
+// bytes with ~1/3 of the VALU and 23 instead of 32 stores:
+//  * every store's byte offset is a per-lane constant (S24Off, computed once per kernel) + the tile's
+//    uniform qt * 32 * stride in the scalar soffset (the descriptor's range check covers voffset + soffset);
+//  * level 1: the two 16-query halves (u) go out in ONE store: lane row g holds level-1 cols 2g, 2g+1 of
+//    both halves; one v_permlane16_swap per value pair hands row 0 the u = 0 cols 2, 3 of row 1 and row 1
+//    the u = 1 cols 0, 1 of row 0 (rows 2, 3 likewise for cols 4-7), so row g writes half u = g & 1, piece
+//    g >> 1 of the 24-byte chunk;
+//  * level 2: the 4 (u, row) chunks of 4 columns, one column per lane row, are a 4 x 4 transpose over the
+//    lane rows (2 permlane32 + 2 permlane16 swaps): lane row r writes chunk r in ONE store;
+//  * level 3: one permlane16 swap sums the column pairs of both halves, one permlane32 swap brings col 1
+//    next to col 0 in rows 0 (u = 0) and 1 (u = 1): one word + short store pair.
+// TAIL (the last, partial query tile only, a uniform branch with the same stores): lanes whose query
+// is past the map add kBig to their offsets (dropped by the range check).
+struct S24Off {
+    unsigned o0[8];            // level 0 M-tile mt, half u = 0 (u = 1: + 16 queries x 24 B)
+    unsigned o1[4];            // level 1 row rp
+    unsigned o2;               // level 2
+    unsigned o3w, o3s;         // level 3 word / short
+    bool odd;                  // level-3 half chunk 2-aligned: short first (uniform)
+};
+
+template <bool TAIL>
+__device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const Lvl (&L)[4], const S24Off& o, int qt,
+                                               int N, int n, int g) {
+    const int q0 = qt * 32;
+    const int s24 = __builtin_amdgcn_readfirstlane(q0 * 24), s12 = __builtin_amdgcn_readfirstlane(q0 * 12);
+    unsigned adj[2] = {0u, 0u}, adj1 = 0u, adj2 = 0u, adj3 = 0u;
+    if constexpr (TAIL) {
+        adj[0] = q0 + n < N ? 0u : kBig;
+        adj[1] = q0 + 16 + n < N ? 0u : kBig;
+        adj1 = adj[g & 1];
+        adj2 = adj[g >> 1];
+        adj3 = adj[g & 1];
+    }
+    // level 0: lane (n, g) holds cols 8 ch + 4 (g & 1) .. + 3 of row 2 rp + (g >> 1): one 12-byte piece
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+            __builtin_amdgcn_raw_buffer_store_b96(
+                pack24g(__float_as_uint(acc[mt][u][0]), __float_as_uint(acc[mt][u][1]), __float_as_uint(acc[mt][u][2]),
+                        __float_as_uint(acc[mt][u][3])),
+                L[0].rsrc, (int)(o.o0[mt] + adj[u] + 384u * u), s24, AUX_NT);
+    // level 1 (values and summation order as epilogue16)
+    float t2[2][2];
+#pragma unroll
+    for (int rp = 0; rp < 4; ++rp) {
+        float s0[2], s1[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const f32x4& a = acc[2 * rp][u];
+            const f32x4& c = acc[2 * rp + 1][u];
+            float x0 = a[0] + a[1], x1 = a[2] + a[3], y0 = c[0] + c[1], y1 = c[2] + c[3];
+            swapf(x0, y0);
+            swapf(x1, y1);
+            s0[u] = x0 + y0;
+            s1[u] = x1 + y1;
+            const float t = s0[u] + s1[u];
+            t2[u][rp >> 1] = (rp & 1) ? t2[u][rp >> 1] + t : t;
+        }
+        unsigned a0 = __float_as_uint(0.25f * s0[0]), b0 = __float_as_uint(0.25f * s0[1]);
+        unsigned a1 = __float_as_uint(0.25f * s1[0]), b1 = __float_as_uint(0.25f * s1[1]);
+        swap16(a0, b0);
+        swap16(a1, b1);
+        __builtin_amdgcn_raw_buffer_store_b96(pack24g(a0, a1, b0, b1), L[1].rsrc, (int)(o.o1[rp] + adj1), s24, AUX_NT);
+    }
+    // level 2: chunk c = 2 u + y2, lane row g holds its col g -> lane row r holds cols 0..3 of chunk r
+    {
+        unsigned v0 = __float_as_uint(0.0625f * t2[0][0]), v1 = __float_as_uint(0.0625f * t2[0][1]);
+        unsigned v2 = __float_as_uint(0.0625f * t2[1][0]), v3 = __float_as_uint(0.0625f * t2[1][1]);
+        swap32(v0, v2);
+        swap32(v1, v3);
+        swap16(v0, v1);
+        swap16(v2, v3);
+        __builtin_amdgcn_raw_buffer_store_b96(pack24g(v0, v1, v2, v3), L[2].rsrc, (int)(o.o2 + adj2), s12, AUX_NT);
+    }
+    // level 3: col x3 of half u = level-2 cols 2 x3, 2 x3 + 1 (lane rows); rows 0 / 1 write halves 0 / 1
+    {
+        unsigned a = __float_as_uint(t2[0][0] + t2[0][1]), b = __float_as_uint(t2[1][0] + t2[1][1]);
+        swap16(a, b);          // row 0: (u0 col-pair of rows 0, 1), row 1: u1 .., row 2 / 3: rows 2, 3
+        const unsigned v = __float_as_uint((1.0f / 64.0f) * (__uint_as_float(a) + __uint_as_float(b)));
+        unsigned c0 = v, c1 = v;
+        swap32(c0, c1);        // c1 of rows 0, 1 = v of rows 2, 3 (col 1)
+        const unsigned r0 = s24_gemm(__uint_as_float(v)), r1 = s24_gemm(__uint_as_float(c1));
+        const bool odd = o.odd;
+        const unsigned word = odd ? __builtin_amdgcn_perm(r1, r0, 0x07060503u) : __builtin_amdgcn_perm(r1, r0, 0x05030201u);
+        const unsigned shrt = odd ? ((r0 >> 8) & 0xffffu) : (r1 >> 16);
+        __builtin_amdgcn_raw_buffer_store_b32((int)word, L[3].rsrc, (int)(o.o3w + adj3), s12, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b16((short)shrt, L[3].rsrc, (int)(o.o3s + adj3), s12, AUX_NT);
+    }
+}
+
 template <int ABL = 0, bool S24 = false>
 __global__ void __launch_bounds__(512, 1)
 corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
@@ -401,6 +525,23 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
         L[l].a = lo32 & 3u;
     }
 
+    S24Off so;
+    if constexpr (S24) {
+        // the per-lane parts of every S24 store offset (epilogue16_s24): query 16 u + n of the tile
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+            so.o0[mt] = (unsigned)n * 24u + 12u * (gq & 1) + soff(L[0], 2 * (mt >> 1) + (gq >> 1), mt & 1);
+#pragma unroll
+        for (int rp = 0; rp < 4; ++rp)
+            so.o1[rp] = (unsigned)(16 * (gq & 1) + n) * 24u + 12u * (gq >> 1) + soff(L[1], rp, 0);
+        so.o2 = (unsigned)(16 * (gq >> 1) + n) * 12u + soff(L[2], gq & 1, 0);
+        const unsigned b3 = soff(L[3], 0, 0);
+        const bool odd = ((b3 + L[3].a) & 2u) != 0;                // uniform: 12 q is a multiple of 4
+        const unsigned l3 = gq < 2 ? (unsigned)(16 * gq + n) * 12u + b3 : kBig;
+        so.o3w = l3 + (odd ? 2u : 0u);
+        so.o3s = l3 + (odd ? 0u : 4u);
+        so.odd = odd;
+    }
     unsigned bhi = (unsigned)(gq * 128 + n) * 16u, blo = bhi + 65536u;
     asm volatile("" : "+v"(bhi), "+v"(blo));
     // B of 32-query tile qt: 16-query tiles 2 qt, 2 qt + 1 at bq + qt * 8192 (+ 4096 for the second)
@@ -418,12 +559,12 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
                 rl[s][uu] = *reinterpret_cast<const bf16x8*>(p + uu * 4096 + 512 * s + lo_off);
             }
     }
-    vmcnt_pad_n<S24 ? kEpiStores16 + 1 : kEpiStores16>(pyr);
+    vmcnt_pad_n<S24 ? (RMD_X3_S24_R05 ? kEpiStores16 + 1 : kEpiStoresS24) : kEpiStores16>(pyr);
     // ping-pong phases as corr_pyramid_x3: waves w and w + 4 of each SIMD alternate MFMA and epilogue
     const int nmax = (nqt + WAVES - 1) / WAVES;
     const int nw = qt < nqt ? (nqt - qt + WAVES - 1) / WAVES : 0;
     const bool late = w >= 4;
-    if (late) __builtin_amdgcn_s_barrier();
+    if (late && ABL < 3) __builtin_amdgcn_s_barrier();
     for (int k = 0; k < nmax; ++k) {
         const int qn = qt + WAVES;
         if (k < nw) {
@@ -432,16 +573,26 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
             read_a16<0, 0>(a0, smem, bhi, blo);
             ksteps16<0>(acc, a0, a1, rh, rl, smem, bhi, blo, bq + (size_t)qt * 8192, bq + (size_t)min(qn, nqt - 1) * 8192,
                         lo_off);
-            __builtin_amdgcn_s_barrier();
-            epilogue16<S24>(acc, L, qt, N, n, gq);
-            __builtin_amdgcn_s_barrier();
-        } else {
+            if (ABL < 3) __builtin_amdgcn_s_barrier();
+            if constexpr (ABL >= 2) {
+#pragma unroll
+                for (int mt = 0; mt < 8; ++mt) asm volatile("" ::"v"(acc[mt][0]), "v"(acc[mt][1]));
+            } else if constexpr (S24 && !RMD_X3_S24_R05) {
+                if (qt * 32 + 32 <= N)
+                    epilogue16_s24<false>(acc, L, so, qt, N, n, gq);
+                else
+                    epilogue16_s24<true>(acc, L, so, qt, N, n, gq);
+            } else {
+                epilogue16<S24>(acc, L, qt, N, n, gq);
+            }
+            if (ABL < 3) __builtin_amdgcn_s_barrier();
+        } else if (ABL < 3) {
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_s_barrier();
         }
         qt = qn;
     }
-    if (!late) __builtin_amdgcn_s_barrier();
+    if (!late && ABL < 3) __builtin_amdgcn_s_barrier();
 }
 
 }  // namespace

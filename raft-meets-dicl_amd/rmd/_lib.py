@@ -95,7 +95,11 @@ _SIGS = {
     "rmd_softargmax_backward": (_I, [_P, _P, _I, _I, _I, _I, _I, ctypes.c_float, _P, _P]),
     "rmd_last_error": (ctypes.c_char_p, []),
     "rmd_version": (ctypes.c_char_p, []),
+    "rmd_abi_version": (_I, []),
 }
+
+# include/rmd.h RMD_ABI_VERSION this binding's signatures (_SIGS) were written for
+ABI_VERSION = 2
 
 
 def lib():
@@ -110,6 +114,9 @@ def lib():
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args
+        if l.rmd_abi_version() != ABI_VERSION:
+            raise RmdError(f"rmd: {LIB_PATH} implements ABI {l.rmd_abi_version()}, this binding needs "
+                           f"ABI {ABI_VERSION} (include/rmd.h RMD_ABI_VERSION); rebuild the library")
         _lib = l
     return _lib
 

@@ -101,12 +101,34 @@ def current():
     return _current
 
 
-def volume_bytes(batch, height, width, levels, precision, training):
-    """HBM bytes of the all-pairs path for a (batch, height, width) query grid: the pooled pyramid in
-    the precision's storage type, plus the dense fp32 pyramid gradient when training."""
+_ELEMENT_BYTES = {0: 4, 1: 2, 4: 3}     # RMD_F32, RMD_F16, RMD_S24 (include/rmd.h)
+
+
+def pyramid_bytes(batch, height, width, levels, precision, channels=None, gpu=True):
+    """HBM bytes of the pyramid a block of this precision writes, in the storage and layout the call
+    resolves (rmd_pyramid_describe_for): the 24-bit S24 storage of 'fp32' / 'fp32-s24' exists only where
+    the split-bf16 x3 GEMM runs (a GPU block, C <= 256, every S24 level slab < 2 GiB) — elsewhere the
+    pyramid is F32, a third larger; the bf16 GEMM's tiles layout pads odd heights.  Without
+    the channel count the S24 modes are charged F32 bytes (the larger of the two)."""
+    from . import _lib, ops                  # lazy: no import-time dependency on the library
+    compute, storage = ops.PRECISIONS[precision]
+    if storage == _lib.RMD_S24 and (not gpu or channels is None):
+        storage = _lib.RMD_F32                # CPU kernels store F32; unknown C: the larger storage
+    if gpu and channels is not None:
+        d = _lib.describe_for(batch, height, width, levels, storage, channels, compute)
+    else:
+        d = _lib.describe(batch, height, width, levels, storage)
+    return d.total_elements * _ELEMENT_BYTES[d.storage]
+
+
+def volume_bytes(batch, height, width, levels, precision, training, channels=None, gpu=True):
+    """HBM bytes of the all-pairs path for a (batch, height, width) query grid: the pooled pyramid in the
+    storage the call resolves (pyramid_bytes), plus the dense fp32 pyramid gradient when training.  A
+    training block also keeps each lookup's fp32 gradient until the pyramid backward, up to
+    rmd.ops.GRAD_PENDING_BYTES (1 GiB) before they are folded into G — at most that much more."""
     n = height * width
     t = sum((height >> l) * (width >> l) for l in range(levels))
-    b = batch * n * t * _STORAGE_BYTES[precision]
+    b = pyramid_bytes(batch, height, width, levels, precision, channels, gpu)
     if training:
         b += batch * n * (t + 8 * levels * height) * 4          # G over the 8-padded target rows
     return b
@@ -115,11 +137,13 @@ def volume_bytes(batch, height, width, levels, precision, training):
 OTF_BACKWARD_MAX_CHANNELS = 256       # rmd_corr_otf_backward's limit (include/rmd.h)
 
 
-def choose_method(method, batch, height, width, levels, precision, training, budget, channels=None):
+def choose_method(method, batch, height, width, levels, precision, training, budget, channels=None, gpu=True):
     """'volume' or 'otf' for a block: explicit methods pass through; 'auto' takes the volume while it
-    fits the budget.  A training block with more than 256 channels has no on-the-fly backward: 'auto'
-    keeps the volume for it and an explicit 'otf' raises here, at construction, instead of in backward."""
-    otf_trainable = not training or channels is None or channels <= OTF_BACKWARD_MAX_CHANNELS
+    fits the budget (volume_bytes, with the storage resolved for `channels` on a GPU block).  A GPU
+    training block with more than 256 channels has no on-the-fly backward: 'auto' keeps the volume for
+    it and an explicit 'otf' raises here, at construction, instead of in backward (the CPU kernels
+    train any channel count)."""
+    otf_trainable = not training or not gpu or channels is None or channels <= OTF_BACKWARD_MAX_CHANNELS
     if method == "otf" and not otf_trainable:
         raise ValueError(f"corr-method 'otf' cannot train a block with {channels} channels "
                          f"(the on-the-fly backward supports C <= {OTF_BACKWARD_MAX_CHANNELS}); use 'volume'")
@@ -127,4 +151,5 @@ def choose_method(method, batch, height, width, levels, precision, training, bud
         return method
     if not otf_trainable:
         return "volume"
-    return "otf" if volume_bytes(batch, height, width, levels, precision, training) > budget else "volume"
+    vb = volume_bytes(batch, height, width, levels, precision, training, channels, gpu)
+    return "otf" if vb > budget else "volume"

@@ -289,6 +289,10 @@ GRAD_BUILD = True
 # bf16 modes: G written as bfloat16 by the build and read by the bf16-B grad GEMMs (bit-identical to
 # the fp32 G, whose GEMM rounds it to bfloat16 on load; half the G traffic).  False: fp32 G (A/B only)
 GRAD_BF16 = True
+# The pending lookup gradients are fp32 (B, L (2r+1)^2, H, W) tensors kept alive until the pyramid
+# backward (cfg2 b8, r = 4: 73 MB each, 0.88 GB for 12 lookups).  Past this many bytes they are folded
+# into an fp32 G early (the build accumulates in lookup order, so G is the same sums) and released.
+GRAD_PENDING_BYTES = 1 << 30
 
 
 class _CorrState:
@@ -310,15 +314,20 @@ def _mask_bits(mask_costs, levels):
 
 
 def _build_grad(st, bf16=False):
-    """G from the pending lookup gradients (rmd_corr_grad_build), consecutive equal radii per launch;
-    bf16: one launch writes a bfloat16 G (the caller checked one radius, <= 16 lookups)."""
+    """G from the pending lookup gradients (rmd_corr_grad_build), consecutive equal radii per launch,
+    added to the fp32 G of an earlier flush if there is one; bf16: one launch writes a bfloat16 G (the
+    caller checked one radius, <= 16 lookups, no earlier flush)."""
     d = st.pyr.desc
     lib = _lib.lib()
     t = lib.rmd_corr_grad_targets(d.height, d.width, d.levels)
     pend, st.pending = st.pending, []
     dev = pend[0][0].device
-    G = torch.empty(d.batch * d.height * d.width * t, dtype=torch.bfloat16 if bf16 else torch.float32, device=dev)
+    G = st.grad
+    if G is None:
+        G = torch.empty(d.batch * d.height * d.width * t, dtype=torch.bfloat16 if bf16 else torch.float32,
+                        device=dev)
     i = 0
+    acc0 = 1 if st.grad is not None else 0
     with torch.cuda.device(dev):
         stream = _stream(G)
         while i < len(pend):
@@ -330,7 +339,7 @@ def _build_grad(st, bf16=False):
             cos = (ctypes.c_void_p * len(grp))(*[x[1].data_ptr() for x in grp])
             masks = (ctypes.c_uint * len(grp))(*[x[3] for x in grp])
             _lib.check(lib.rmd_corr_grad_build_ex(gouts, cos, masks, len(grp), ctypes.byref(d), grp[0][2],
-                                                  1 if i > 0 else 0, 1 if bf16 else 0, _ptr(G), stream),
+                                                  1 if i > 0 else acc0, 1 if bf16 else 0, _ptr(G), stream),
                        "rmd_corr_grad_build")
             i = j
     return G
@@ -353,7 +362,7 @@ class _CorrPyramidFn(torch.autograd.Function):
         levels = st.pyr.levels
         bf16_mode = PRECISIONS[st.precision][0] == RMD_BF16
         if st.pending:
-            one_launch = len(st.pending) <= 16 and len({x[2] for x in st.pending}) == 1
+            one_launch = len(st.pending) <= 16 and len({x[2] for x in st.pending}) == 1 and st.grad is None
             st.grad = _build_grad(st, bf16=GRAD_BF16 and bf16_mode and one_launch)
         if st.grad is None:
             return torch.zeros_like(f1), torch.zeros_like(f2), None
@@ -413,6 +422,8 @@ class _CorrLookupFn(torch.autograd.Function):
         if GRAD_BUILD:
             # G is written from every lookup's gradient at once by the pyramid backward
             st.pending.append((g, co, ctx.radius, ctx.mask))
+            if sum(x[0].numel() for x in st.pending) * 4 > GRAD_PENDING_BYTES:
+                st.grad = _build_grad(st)         # fp32 G, accumulated from here on
             return gout.new_zeros(()), None, None, None, None
         d = st.pyr.desc
         lib = _lib.lib()

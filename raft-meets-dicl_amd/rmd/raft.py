@@ -40,9 +40,10 @@ class CorrBlock:
         tokens = training and fmap1.is_cuda
         b, c, h, w = fmap1.shape
         # the C <= 256 limit of the on-the-fly backward is the HIP kernel's (rmd_corr_otf_backward):
-        # the CPU kernels train any channel count, so only a GPU training block is steered by it
+        # the CPU kernels train any channel count, so only a GPU training block is steered by it; the
+        # volume's bytes are those of the storage this (device, C) resolves to
         self.method = config.choose_method(opts.method, b, h, w, num_levels, self.precision, training,
-                                           opts.memory_budget, channels=c if tokens else None)
+                                           opts.memory_budget, channels=c, gpu=fmap1.is_cuda)
         scale = float(c) ** -0.5 if self.scale is None else float(self.scale)
         if self.method == "otf":
             self.pyramid = None

@@ -51,3 +51,12 @@ def assert_close_elementwise(got, ref, rtol, atol):
         k = int(np.argmax(err - lim))
         raise AssertionError(f"elementwise tolerance exceeded at flat {k}: got {got[fin][k]!r} ref {ref[fin][k]!r} "
                              f"err {err[k]:.3e} > {lim[k]:.3e} ({int((err > lim).sum())} of {err.size} entries)")
+
+
+def assert_fp32_gate(got, ref):
+    """north_star's fp32 cost-volume gate applied per element: |got - ref| <= 1e-4 |ref| + 1e-5 max|ref|
+    (max over the finite reference entries; NaN patterns must match)."""
+    ref = np.asarray(ref, dtype=np.float64)
+    fin = np.isfinite(ref)
+    scale = float(np.abs(ref[fin]).max()) if fin.any() else 0.0
+    assert_close_elementwise(got, ref, rtol=1e-4, atol=1e-5 * scale)

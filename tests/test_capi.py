@@ -32,6 +32,15 @@ def test_version():
     assert _lib.lib().rmd_version().startswith(b"rmd ")
 
 
+def test_abi_version_matches_header_and_binding():
+    """the rmd_corr_grad_gemm signature change is ABI 2; the header, the library and the
+    ctypes binding agree on it, and the binding refuses a library of another ABI."""
+    from rmd import _lib
+    m = re.search(r"#define RMD_ABI_VERSION (\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == _lib.lib().rmd_abi_version() == 2
+    assert _lib.lib().rmd_version().endswith(b"abi 2")
+
+
 def test_describe_cfg2_geometry():
     from rmd import _lib
     d = _lib.describe(8, 55, 128, 4, _lib.RMD_F16)

@@ -78,3 +78,25 @@ def test_configure_restore():
     finally:
         config.restore(prev)
     assert config.current() == prev
+
+
+def test_volume_bytes_resolve_the_pyramid_storage():
+    """'fp32' stores S24 (3 bytes) only where the x3 GEMM runs; C > 256, a level slab of
+    >= 2 GiB (large maps) and CPU blocks store F32, and the budget must charge those 4 bytes."""
+    from rmd import _lib
+    tot = _lib.describe(8, 55, 128, 4, _lib.RMD_F32).total_elements
+    assert config.pyramid_bytes(8, 55, 128, 4, "fp32", channels=256) == 3 * tot
+    assert config.pyramid_bytes(8, 55, 128, 4, "fp32", channels=320) == 4 * tot       # tiled f32 GEMM
+    assert config.pyramid_bytes(8, 55, 128, 4, "fp32", channels=256, gpu=False) == 4 * tot
+    assert config.pyramid_bytes(8, 55, 128, 4, "fp32") == 4 * tot                     # C unknown: larger
+    assert config.pyramid_bytes(8, 55, 128, 4, "fp32-f32", channels=256) == 4 * tot
+    # bf16: the w8 GEMM's tiles layout (odd H pads level-0/1 chunk rows)
+    tiles = _lib.describe_for(8, 55, 128, 4, _lib.RMD_F16, 256, _lib.RMD_BF16)
+    assert config.pyramid_bytes(8, 55, 128, 4, "bf16", channels=256) == 2 * tiles.total_elements > 2 * tot
+    big = _lib.describe(1, 270, 480, 4, _lib.RMD_F32).total_elements                 # 4K 1/8 map
+    assert config.pyramid_bytes(1, 270, 480, 4, "fp32", channels=256) == 4 * big
+    # a budget between the S24 and the F32 size: auto keeps the volume only where S24 applies
+    budget = int(3.5 * tot)
+    assert config.choose_method("auto", 8, 55, 128, 4, "fp32", False, budget, channels=256) == "volume"
+    assert config.choose_method("auto", 8, 55, 128, 4, "fp32", False, budget, channels=320) == "otf"
+    assert config.choose_method("auto", 8, 55, 128, 4, "fp32", False, budget, channels=256, gpu=False) == "otf"

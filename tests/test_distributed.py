@@ -98,11 +98,13 @@ def _inputs(b, seed):
     return img1, img2, co
 
 
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, q, device="cuda"):
     sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
+    if device == "cpu":
+        torch.set_num_threads(1)
     _init(rank, world, port)
     try:
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", 0) if device == "cuda" else torch.device("cpu")
         net = torch.nn.parallel.DistributedDataParallel(_TinyCorrNet().to(dev))
         img1, img2, co = (t.to(dev) for t in _inputs(4, 10 + rank))
         net(img1, img2, co).backward()
@@ -111,12 +113,11 @@ def _ddp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-def test_ddp_gradient_allreduce_through_corr_autograd():
+def _ddp_check(world, device):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q, device)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
@@ -124,12 +125,12 @@ def test_ddp_gradient_allreduce_through_corr_autograd():
         p.join(timeout=60)
         assert p.exitcode == 0
     sys.path.insert(0, os.path.join(ROOT, "raft-meets-dicl_amd"))
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", 0) if device == "cuda" else torch.device("cpu")
     net = _TinyCorrNet().to(dev)
     loss = 0.0
-    for r in range(2):                 # mean over ranks of each rank's loss == DDP's averaged gradient
+    for r in range(world):             # mean over ranks of each rank's loss == DDP's averaged gradient
         img1, img2, co = (t.to(dev) for t in _inputs(4, 10 + r))
-        loss = loss + 0.5 * net(img1, img2, co)
+        loss = loss + net(img1, img2, co) / world
     loss.backward()
     ref_w = net.enc.weight.grad.cpu().numpy()
     ref_b = net.enc.bias.grad.cpu().numpy()
@@ -139,7 +140,21 @@ def test_ddp_gradient_allreduce_through_corr_autograd():
     assert np.abs(ref_w).max() > 0
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_ddp_gradient_allreduce_through_corr_autograd(world):
+    """world ranks share cuda:0 over gloo: the HIP correlation forward/backward under DDP."""
+    _ddp_check(world, "cuda")
+
+
+@pytest.mark.parametrize("world", [4])
+def test_ddp_gradient_allreduce_through_corr_autograd_cpu(world):
+    """The same DDP gradient check on CPU tensors (the operators' CPU kernels, rmd/cpu.py) at world 4:
+    the bucketed all-reduce over the correlation autograd, rehearsed without a GPU."""
+    _ddp_check(world, "cpu")
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_launches_its_own_ranks(world):
     """`bench.py --gpus N` started as one plain process spawns N ranks through
     torch.distributed.run (the same launcher the driver uses) and reports n_gpus = the world size

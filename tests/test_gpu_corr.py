@@ -5,8 +5,8 @@ float64 CPU oracle at the same seeded inputs, and (3) at the full cfg2 size (B=8
 against the oracle on a random sample of queries plus determinism.
 
 Tolerances (max|got-ref| / max|ref|, conftest.rel_max_err):
-  * fp32 mode (split-bf16 MFMA hi.hi + hi.lo + lo.hi, f32 pyramid) and fp32-exact (exact f32 MFMA):
-    1e-4 — north_star's cost-volume gate
+  * fp32 modes (split-bf16 MFMA hi.hi + hi.lo + lo.hi; fp32-exact: exact f32 MFMA): 1e-4 — north_star's
+    cost-volume gate — and, per element, |err| <= 1e-4 |ref| + 1e-5 max|ref| (conftest.assert_fp32_gate)
   * bf16 mode (bf16 operands, f32 accumulation, fp16 pyramid): 1e-2 — operand rounding 2^-9
 """
 
@@ -15,7 +15,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import assert_close_elementwise, load_golden, rel_max_err
+from conftest import assert_close_elementwise, assert_fp32_gate, load_golden, rel_max_err
 
 pytestmark = pytest.mark.gpu
 
@@ -42,6 +42,8 @@ def test_corr_block_matches_reference_golden(name, precision):
     assert out.dtype == torch.float32 and out.is_contiguous()
     assert tuple(out.shape) == g["out"].shape
     assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
+    if precision.startswith("fp32") and precision != "fp32-f16":
+        assert_fp32_gate(out.cpu().numpy(), g["out"])
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32-exact", 1e-5), ("fp32", 1e-4), ("fp32-f32", 1e-4)])
@@ -52,9 +54,10 @@ def test_pyramid_levels_match_reference_golden(precision, tol):
     for i, lvl in enumerate(cb.corr_pyramid):
         assert tuple(lvl.shape) == g[f"pyr{i}"].shape
         assert rel_max_err(lvl.cpu().numpy(), g[f"pyr{i}"]) < tol
+        assert_fp32_gate(lvl.cpu().numpy(), g[f"pyr{i}"])
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-f32", "fp32-exact", "bf16"])
 def test_cfg1_shape_matches_oracle(precision):
     """cfg1 feature shape (368x496 -> 46x62), C=256, B=1, full oracle comparison."""
     import rmd
@@ -68,6 +71,8 @@ def test_cfg1_shape_matches_oracle(precision):
     ref = oracle.corr_lookup(oracle.corr_pyramid(f1.astype(np.float64), f2.astype(np.float64), 4),
                              co.astype(np.float64), 4)
     assert rel_max_err(out, ref) < TOL[precision]
+    if precision.startswith("fp32"):
+        assert_fp32_gate(out, ref)
 
 
 @pytest.mark.parametrize("radius", [1, 2, 3, 5, 6, 8])
@@ -265,6 +270,8 @@ def test_raft_fs_corr_block_matches_reference_golden(precision):
     out = cb(_t(g["coords"]))
     assert out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == g["out"].shape
     assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
+    if precision.startswith("fp32") and precision != "fp32-f16":
+        assert_fp32_gate(out.cpu().numpy(), g["out"])
 
 
 def test_dot_correlation_module_matches_reference_golden():

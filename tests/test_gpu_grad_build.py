@@ -232,3 +232,34 @@ def test_autograd_bf16_mode_bf16_g_matches_fp32_g():
     a1, a2 = grads(True)
     s1, s2 = grads(False)
     assert torch.isfinite(a1).all() and torch.equal(a1, s1) and torch.equal(a2, s2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_autograd_pending_flush_matches_single_build(precision):
+    """past ops.GRAD_PENDING_BYTES of kept lookup gradients the lookups are folded into an
+    fp32 G early (accumulate launches, same lookup order).  With the threshold at one byte every lookup
+    backward flushes: the gradients are bit-identical to one build at the pyramid backward (bf16 mode:
+    the bfloat16 G is the rounded fp32 G, which its GEMM rounds on load, so equal there too)."""
+    import rmd
+    from rmd import ops
+    rng = np.random.default_rng(21)
+    b, c, h, w = 2, 64, 23, 40
+    f1 = torch.tensor(rng.standard_normal((b, c, h, w)), dtype=torch.float32, device="cuda")
+    f2 = torch.tensor(rng.standard_normal((b, c, h, w)), dtype=torch.float32, device="cuda")
+    lk = _inputs(b, h, w, 4, 4, 5, seed=8)
+
+    def grads(limit):
+        old = ops.GRAD_PENDING_BYTES
+        ops.GRAD_PENDING_BYTES = limit
+        try:
+            t1, t2 = f1.clone().requires_grad_(True), f2.clone().requires_grad_(True)
+            cb = rmd.raft.CorrBlock(t1, t2, 4, 4, precision=precision)
+            loss = sum((cb(co) * go).sum() for go, co in lk)
+            loss.backward()
+            return t1.grad, t2.grad
+        finally:
+            ops.GRAD_PENDING_BYTES = old
+
+    a1, a2 = grads(1 << 40)
+    s1, s2 = grads(1)
+    assert torch.isfinite(a1).all() and torch.equal(a1, s1) and torch.equal(a2, s2)

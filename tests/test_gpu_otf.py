@@ -9,7 +9,8 @@ full cfg2 size against the volume path (same kernels' results must agree).  The 
 (gen_golden_fs_backward.py), the float64 oracle over several lookups, and the volume path's backward.
 
 Tolerances (max|got-ref| / max|ref|): fp32 mode (split-bf16 MFMA, ~1e-5) and fp32-exact (f32 MFMA) 1e-4,
-bf16 mode 1e-2.
+bf16 mode 1e-2; the forward fp32 modes also per element, |err| <= 1e-4 |ref| + 1e-5 max|ref|
+(conftest.assert_fp32_gate).
 """
 
 import numpy as np
@@ -17,7 +18,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import load_golden, rel_max_err
+from conftest import assert_fp32_gate, load_golden, rel_max_err
 
 pytestmark = pytest.mark.gpu
 
@@ -46,6 +47,8 @@ def test_otf_matches_reference_golden(precision, name):
     torch.cuda.synchronize()
     assert out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == g["out"].shape
     assert rel_max_err(out.cpu().numpy(), g["out"]) < TOL[precision]
+    if precision.startswith("fp32"):
+        assert_fp32_gate(out.cpu().numpy(), g["out"])
 
 
 CASES = [
@@ -78,6 +81,8 @@ def test_otf_matches_oracle(case, precision):
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     fin = ~np.isnan(ref)
     assert rel_max_err(got[fin], ref[fin]) < TOL[precision]
+    if precision.startswith("fp32"):
+        assert_fp32_gate(got, ref)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32-exact", "bf16"])
@@ -261,6 +266,37 @@ def test_otf_backward_deterministic_across_wide_dynamic_range(precision):
                    f1, f2, cos, gos)[1:] for _ in range(3)]
     for g1, g2 in runs[1:]:
         assert np.array_equal(g1, runs[0][0]) and np.array_equal(g2, runs[0][1])
+    r1 = np.zeros(f1.shape)
+    r2 = np.zeros(f2.shape)
+    for co, go in zip(cos, gos):
+        a1, a2 = oracle.corr_lookup_fs_backward(f1.astype(np.float64), f2.astype(np.float64), co.astype(np.float64),
+                                                levels, r, go.astype(np.float64), ())
+        r1 += a1
+        r2 += a2
+    assert rel_max_err(runs[0][0], r1) < TOL[precision]
+    assert rel_max_err(runs[0][1], r2) < TOL[precision]
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_otf_backward_bound_beyond_float_range(precision):
+    """the fixed-point exponent's bound records x N x max|w| x max|q~| exceeds FLT_MAX
+    (upstream gradients ~1e31, features ~1e3 at a 48 x 80 map: ~1e39) while every gradient stays finite.
+    The bound is formed in double, so s is chosen for it (a float bound overflowed to inf and took s = 60,
+    overflowing every int64 sum); gradients finite, run-to-run equal, and at the float64 oracle."""
+    import rmd
+    rng = np.random.default_rng(31)
+    b, c, h, w, levels, r = 1, 32, 48, 80, 2, 3
+    f1 = (rng.standard_normal((b, c, h, w)) * 1e3).astype(np.float32)
+    f2 = (rng.standard_normal((b, c, h, w)) * 1e3).astype(np.float32)
+    cos = [_grid_coords(rng, b, h, w, 1.5) for _ in range(2)]
+    d = (2 * r + 1) ** 2
+    gos = [(rng.standard_normal((b, levels * d, h, w)) * 1e31).astype(np.float32) for _ in range(2)]
+    qmax = float(np.abs(f1).max())                       # raft_fs: q~ = fmap1 (scale 1)
+    assert 2 * h * w * float(np.abs(gos[0]).max()) * qmax > np.finfo(np.float32).max
+    runs = [_grads(lambda a, bb: rmd.raft_fs.CorrBlock(a, bb, levels, r, precision=precision, method="otf"),
+                   f1, f2, cos, gos)[1:] for _ in range(2)]
+    assert np.isfinite(runs[0][0]).all() and np.isfinite(runs[0][1]).all()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
     r1 = np.zeros(f1.shape)
     r2 = np.zeros(f2.shape)
     for co, go in zip(cos, gos):
