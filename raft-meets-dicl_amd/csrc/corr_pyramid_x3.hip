@@ -130,7 +130,22 @@ struct Lvl {
     int rows;         // valid rows of this block on the level
     int chunks;       // valid chunks of this block's rows (level 0: 0..2, others 0..1)
     unsigned a;       // base address mod 4 (S24 level 3 aligns its word store with it)
+    unsigned long long base;    // descriptor base address and byte range (epilogue16_s24 rebases them
+    unsigned range;             // per query tile)
 };
+
+// L's descriptor moved `delta` bytes forward (range shrunk to match): SALU work per tile, so the stores
+// keep a zero soffset — with an SGPR soffset the compiler omits the wait state a > 8-byte store needs
+// before a VALU overwrites its data VGPRs (LLVM's MUBUF store-data hazard rule exempts register soffsets),
+// and on gfx950 that corrupted the last lanes of the store whose data registers the next VALU reused
+// (round-6 debug: tools/s24_debug.py)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rebase(const Lvl& L, unsigned delta) {
+    const unsigned long long p = L.base + delta;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p), hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+    const unsigned r = __builtin_amdgcn_readfirstlane(L.range > delta ? L.range - delta : 0u);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, (int)r,
+                                             0x00020000);
+}
 
 __device__ __forceinline__ unsigned soff(const Lvl& L, int row, int chunk) {
     return (row < L.rows && chunk < L.chunks) ? (unsigned)row * L.rs + (unsigned)chunk * L.cs : kBig;
@@ -360,8 +375,8 @@ __device__ __forceinline__ void epilogue16(const f32x4 (&acc)[8][2], const Lvl (
 // 384 MFMAs, whose issue gaps hold ~2 VALU each, so it stretched the MFMA phase and held the clock down
 // (profiles/x3_epi_r06.json).  This one computes the same values in the same order and stores the same
 // bytes with ~1/3 of the VALU and 23 instead of 32 stores:
-//  * every store's byte offset is a per-lane constant (S24Off, computed once per kernel) + the tile's
-//    uniform qt * 32 * stride in the scalar soffset (the descriptor's range check covers voffset + soffset);
+//  * every store's byte offset is a per-lane constant (S24Off, computed once per kernel) from a descriptor
+//    rebased by the tile's uniform qt * 32 * stride (SALU: rebase);
 //  * level 1: the two 16-query halves (u) go out in ONE store: lane row g holds level-1 cols 2g, 2g+1 of
 //    both halves; one v_permlane16_swap per value pair hands row 0 the u = 0 cols 2, 3 of row 1 and row 1
 //    the u = 1 cols 0, 1 of row 0 (rows 2, 3 likewise for cols 4-7), so row g writes half u = g & 1, piece
@@ -384,7 +399,9 @@ template <bool TAIL>
 __device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const Lvl (&L)[4], const S24Off& o, int qt,
                                                int N, int n, int g) {
     const int q0 = qt * 32;
-    const int s24 = __builtin_amdgcn_readfirstlane(q0 * 24), s12 = __builtin_amdgcn_readfirstlane(q0 * 12);
+    const unsigned d24 = (unsigned)q0 * 24u, d12 = (unsigned)q0 * 12u;
+    const __amdgpu_buffer_rsrc_t r0 = rebase(L[0], d24), r1 = rebase(L[1], d24), r2 = rebase(L[2], d12),
+                                 r3 = rebase(L[3], d12);
     unsigned adj[2] = {0u, 0u}, adj1 = 0u, adj2 = 0u, adj3 = 0u;
     if constexpr (TAIL) {
         adj[0] = q0 + n < N ? 0u : kBig;
@@ -401,7 +418,7 @@ __device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const L
             __builtin_amdgcn_raw_buffer_store_b96(
                 pack24g(__float_as_uint(acc[mt][u][0]), __float_as_uint(acc[mt][u][1]), __float_as_uint(acc[mt][u][2]),
                         __float_as_uint(acc[mt][u][3])),
-                L[0].rsrc, (int)(o.o0[mt] + adj[u] + 384u * u), s24, AUX_NT);
+                r0, (int)(o.o0[mt] + adj[u] + 384u * u), 0, AUX_NT);
     // level 1 (values and summation order as epilogue16)
     float t2[2][2];
 #pragma unroll
@@ -423,7 +440,7 @@ __device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const L
         unsigned a1 = __float_as_uint(0.25f * s1[0]), b1 = __float_as_uint(0.25f * s1[1]);
         swap16(a0, b0);
         swap16(a1, b1);
-        __builtin_amdgcn_raw_buffer_store_b96(pack24g(a0, a1, b0, b1), L[1].rsrc, (int)(o.o1[rp] + adj1), s24, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b96(pack24g(a0, a1, b0, b1), r1, (int)(o.o1[rp] + adj1), 0, AUX_NT);
     }
     // level 2: chunk c = 2 u + y2, lane row g holds its col g -> lane row r holds cols 0..3 of chunk r
     {
@@ -433,7 +450,7 @@ __device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const L
         swap32(v1, v3);
         swap16(v0, v1);
         swap16(v2, v3);
-        __builtin_amdgcn_raw_buffer_store_b96(pack24g(v0, v1, v2, v3), L[2].rsrc, (int)(o.o2 + adj2), s12, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b96(pack24g(v0, v1, v2, v3), r2, (int)(o.o2 + adj2), 0, AUX_NT);
     }
     // level 3: col x3 of half u = level-2 cols 2 x3, 2 x3 + 1 (lane rows); rows 0 / 1 write halves 0 / 1
     {
@@ -446,28 +463,27 @@ __device__ __forceinline__ void epilogue16_s24(const f32x4 (&acc)[8][2], const L
         const bool odd = o.odd;
         const unsigned word = odd ? __builtin_amdgcn_perm(r1, r0, 0x07060503u) : __builtin_amdgcn_perm(r1, r0, 0x05030201u);
         const unsigned shrt = odd ? ((r0 >> 8) & 0xffffu) : (r1 >> 16);
-        __builtin_amdgcn_raw_buffer_store_b32((int)word, L[3].rsrc, (int)(o.o3w + adj3), s12, AUX_NT);
-        __builtin_amdgcn_raw_buffer_store_b16((short)shrt, L[3].rsrc, (int)(o.o3s + adj3), s12, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b32((int)word, r3, (int)(o.o3w + adj3), 0, AUX_NT);
+        __builtin_amdgcn_raw_buffer_store_b16((short)shrt, r3, (int)(o.o3s + adj3), 0, AUX_NT);
     }
 }
 
-template <int ABL = 0, bool S24 = false>
-__global__ void __launch_bounds__(512, 1)
-corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
-                 const __bf16* __restrict__ bLo, PyrGeom g, int units, unsigned char* __restrict__ pyr) {
+// One segment of a workgroup's work: target block tb of image b against query tiles [qlo, qhi).  Every
+// wave runs 2 ceil((qhi - qlo) / 8) + 1 barriers; after the last one no wave reads LDS any more, so the
+// next segment may restage A at once.
+template <int ABL, bool S24>
+__device__ __forceinline__ void x3_segment(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
+                                           const __bf16* __restrict__ bHi, const __bf16* __restrict__ bLo,
+                                           const PyrGeom& g, unsigned char* __restrict__ pyr, unsigned char* smem,
+                                           int b, int tb, int qlo, int qhi) {
     constexpr unsigned E = S24 ? 3u : 4u;                  // bytes per stored element
     constexpr int WAVES = 8;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int H = g.height, W = g.width, N = H * W;
     const int ncb = (W + kBlockCols - 1) / kBlockCols;
-    const int nblk = ((H + kBlockRows - 1) / kBlockRows) * ncb;
     const int nqt = (N + 31) >> 5;
-    const int u = xcd_block(blockIdx.x, gridDim.x);
-    if (u >= units) return;                                        // uniform per workgroup
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n = lane & 15, gq = lane >> 4;
-    const int b = u / nblk, tb = u - b * nblk;
     const int rb = tb / ncb, cb = tb - rb * ncb;
     const int ty0 = rb * kBlockRows, tx0 = cb * kBlockCols;
 
@@ -523,6 +539,8 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
         L[l].rows = __builtin_amdgcn_readfirstlane(rows);
         L[l].chunks = __builtin_amdgcn_readfirstlane(lv ? max(0, min(nch, g.tx[l] - xc0)) : 0);
         L[l].a = lo32 & 3u;
+        L[l].base = ((unsigned long long)hi32 << 32) | lo32;
+        L[l].range = __builtin_amdgcn_readfirstlane(ABL == 1 ? 0u : (unsigned)rows * rs);
     }
 
     S24Off so;
@@ -547,9 +565,9 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
     // B of 32-query tile qt: 16-query tiles 2 qt, 2 qt + 1 at bq + qt * 8192 (+ 4096 for the second)
     const __bf16* bq = bHi + ((size_t)b * 2 * nqt * 512 + lane) * 8;
     const size_t lo_off = (size_t)(bLo - bHi);
-    int qt = w;
+    int qt = qlo + w;
     bf16x8 rh[kDR16][2], rl[kDR16][2];
-    if (qt < nqt) {
+    if (qt < qhi) {
         const __bf16* p = bq + (size_t)qt * 8192;
 #pragma unroll
         for (int s = 0; s < kDR16 - 1; ++s)
@@ -561,8 +579,8 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
     }
     vmcnt_pad_n<S24 ? (RMD_X3_S24_R05 ? kEpiStores16 + 1 : kEpiStoresS24) : kEpiStores16>(pyr);
     // ping-pong phases as corr_pyramid_x3: waves w and w + 4 of each SIMD alternate MFMA and epilogue
-    const int nmax = (nqt + WAVES - 1) / WAVES;
-    const int nw = qt < nqt ? (nqt - qt + WAVES - 1) / WAVES : 0;
+    const int nmax = (qhi - qlo + WAVES - 1) / WAVES;
+    const int nw = qt < qhi ? (qhi - qt + WAVES - 1) / WAVES : 0;
     const bool late = w >= 4;
     if (late && ABL < 3) __builtin_amdgcn_s_barrier();
     for (int k = 0; k < nmax; ++k) {
@@ -593,6 +611,52 @@ corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo,
         qt = qn;
     }
     if (!late && ABL < 3) __builtin_amdgcn_s_barrier();
+}
+
+// Balanced schedule (round 6).  At cfg2 the 448 (image, block) workgroups of one-CU size run 1.75
+// rounds on 256 CUs: XCD x's 56 blocks take two full workgroup times on its 32 CUs while 8 of them idle
+// half the time.  With bal the grid holds, per XCD, first `full` x wpx whole-block workgroups (one round
+// when full = 1) and then the remaining `rest` blocks cut into `parts` query-tile ranges each, rest x
+// parts a multiple of wpx: hardware dispatch hands each CU that frees up the next workgroup in index
+// order, so every CU runs the same tile count (cfg2: 220 + 3 x 55) and the query tiles in flight on an
+// XCD stay within `parts` offsets (B fragments L2-shared).  A part restages its block's A (from L2).
+struct X3Sched {
+    int bal;      // 0: one workgroup per (image, block), all query tiles
+    int ipx;      // images per XCD
+    int nfull;    // whole-block workgroups per XCD (wpx x full)
+    int parts;    // query-tile parts of each remaining block
+};
+
+template <int ABL = 0, bool S24 = false>
+__global__ void __launch_bounds__(512, 1)
+corr_pyramid_x3s(const __bf16* __restrict__ aHi, const __bf16* __restrict__ aLo, const __bf16* __restrict__ bHi,
+                 const __bf16* __restrict__ bLo, PyrGeom g, int units, X3Sched sc, unsigned char* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ncb = (g.width + kBlockCols - 1) / kBlockCols;
+    const int nblk = ((g.height + kBlockRows - 1) / kBlockRows) * ncb;
+    const int nqt = (g.height * g.width + 31) >> 5;
+    int b, tb, q0 = 0, q1 = nqt;
+    if (!sc.bal) {
+        const int u = xcd_block(blockIdx.x, gridDim.x);
+        if (u >= units) return;                                    // uniform per workgroup
+        b = u / nblk;
+        tb = u - b * nblk;
+    } else {
+        // dispatch deals workgroups round-robin over the 8 XCDs (speed only: every workgroup index
+        // maps to its own piece of work, whatever CU runs it)
+        const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+        int j = k;
+        if (k >= sc.nfull) {
+            const int kk = k - sc.nfull, part = kk % sc.parts;
+            j = sc.nfull + kk / sc.parts;
+            q0 = part * nqt / sc.parts;
+            q1 = (part + 1) * nqt / sc.parts;
+        }
+        const int jb = j / nblk;
+        b = x * sc.ipx + jb;
+        tb = j - jb * nblk;
+    }
+    x3_segment<ABL, S24>(aHi, aLo, bHi, bLo, g, pyr, smem, b, tb, q0, q1);
 }
 
 }  // namespace
@@ -633,6 +697,41 @@ int prepare(const float* f1, const float* f2, int C, float scale, const rmd_pyra
     return check_launch("rmd_corr_prepare/x3");
 }
 
+// RMD_X3_BAL = 0 (A/B builds): always one workgroup per (image, block)
+#ifndef RMD_X3_BAL
+#define RMD_X3_BAL 1
+#endif
+
+// the balanced schedule when every XCD holds the same whole images and one workgroup per (image, block)
+// would leave a partial last round (X3Sched)
+X3Sched schedule(const rmd_pyramid_desc& d, int nblk, int& grid) {
+    X3Sched sc{0, 0, 0, 0};
+    const int units = nblk * d.batch;
+    grid = units;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            cus = v;
+        else
+            cus = -1;
+    }
+    if (!RMD_X3_BAL || cus <= 0 || cus % 8 != 0 || d.batch % 8 != 0) return sc;
+    if (units <= cus || units % cus == 0) return sc;
+    const int wpx = cus / 8, nbx = d.batch / 8 * nblk;
+    const int full = nbx / wpx, rest = nbx - full * wpx;
+    int parts = 1;
+    while ((rest * parts) % wpx != 0) ++parts;
+    const int nqt = (d.height * d.width + 31) / 32;
+    if (parts > 8 || nqt < 8 * parts) return sc;              // pieces too small to pay their A restage
+    sc.bal = 1;
+    sc.ipx = d.batch / 8;
+    sc.nfull = full * wpx;
+    sc.parts = parts;
+    grid = 8 * (sc.nfull + rest * parts);
+    return sc;
+}
+
 int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const int N = d.height * d.width, nqt = (N + 31) / 32;
     const __bf16* aHi = reinterpret_cast<const __bf16*>(ws);
@@ -641,9 +740,12 @@ int pyramid(const rmd_pyramid_desc& d, void* pyr, void* ws, hipStream_t st) {
     const __bf16* bLo = bHi + (size_t)d.batch * nqt * 32 * 256;
     const int nblk = ((d.height + kBlockRows - 1) / kBlockRows) * ((d.width + kBlockCols - 1) / kBlockCols);
     const int units = nblk * d.batch;
+    int grid = units;
+    const X3Sched sc = schedule(d, nblk, grid);
     auto kern = d.storage == RMD_S24 ? corr_pyramid_x3s<RMD_X3_ABL, true> : corr_pyramid_x3s<RMD_X3_ABL, false>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds16);
-    kern<<<units, 512, kLds16, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, reinterpret_cast<unsigned char*>(pyr));
+    kern<<<grid, 512, kLds16, st>>>(aHi, aLo, bHi, bLo, make_geom(d), units, sc,
+                                                          reinterpret_cast<unsigned char*>(pyr));
     return check_launch("rmd_corr_pyramid/gemm-x3");
 }
 

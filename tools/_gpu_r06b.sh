@@ -4,13 +4,17 @@ set -o pipefail
 export TMPDIR=/tmp
 R=gpurun_out/r06b
 mkdir -p $R
+timeout -k 10 120 python3 -u tools/s24_debug.py 2 32 24 40 > $R/s24.txt 2>&1 || { tail -30 $R/s24.txt; exit 1; }
+cat $R/s24.txt
+timeout -k 10 120 python3 -u tools/s24_debug.py 8 256 55 128 > $R/s24b.txt 2>&1 || { tail -30 $R/s24b.txt; exit 1; }
+cat $R/s24b.txt
 timeout -k 10 900 python -u -m pytest tests/test_gpu_corr.py tests/test_gpu_otf.py tests/test_gpu_grad_build.py tests/test_distributed.py tests/test_gpu_e2e.py -m gpu -x -q --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || { tail -40 $R/tests.log; exit 2; }
 tail -3 $R/tests.log
 P=$PWD/raft-meets-dicl_amd/rmd/librmd.so
 AB=$PWD/tools/_ab
 lib() { case $1 in product) echo $P;; *) echo $AB/librmd_$1.so;; esac; }
 for round in 1 2 3; do
-  for v in r05 product x3abl3new; do
+  for v in r05 nobal product; do
     RMD_LIBRARY=$(lib $v) timeout -k 10 120 python3 -u tools/x3_time.py 30 fp32 > $R/t_${v}_$round.json 2> $R/t.err || { tail $R/t.err; exit 3; }
     echo "time $v $(cat $R/t_${v}_$round.json)"
   done
