@@ -847,6 +847,9 @@ def main():
         "metric": "frame-pairs/s @436x1024 RAFT 12 iters (1-8 GPU); corr MFMA% + lookup HBM%",
         "value": world * B * args.steps / elapsed,
         "unit": "frame-pairs/s",
+        "value_scope": ("the cost-volume hot path only (SURVEY §8): correlation GEMM + pooled pyramid + 12 "
+                        "lookups per frame pair, not the whole RAFT network (that figure is "
+                        "model_level.frame_pairs_per_s)"),
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -897,6 +900,9 @@ def main():
                                     "ms_per_step": el32 / args.fp32_steps * 1e3, "steps": args.fp32_steps,
                                     "warmup": 3, "precision": "fp32", "dtype": "fp32",
                                     "pyramid_storage": STORAGE_NAME[storage_bytes("fp32")],
+                                    "storage_note": ("'fp32' mode stores the pyramid as RMD_S24: each fp32 value "
+                                                     "rounded to its top 24 bits (16 significant bits, <= 2^-16 "
+                                                     "relative); 'fp32-f32' keeps 4-byte storage"),
                                     "gemm": "split-bf16 x3 MFMA (hi.hi + hi.lo + lo.hi), fp32 accumulate",
                                     "roofline_gemm": g32, "roofline_lookup": l32}
         del inputs

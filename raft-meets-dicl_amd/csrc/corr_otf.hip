@@ -110,10 +110,6 @@ constexpr int kMaxTasks = 1024;                      // box segments of the MFMA
 #ifndef RMD_OTF_PADS
 #define RMD_OTF_PADS 1
 #endif
-// the row-sweep lookup (otf_sweep_kernel) for C = 256, r <= 4, bf16 / split-bf16: 1 (0: otf_lookup_kernel)
-#ifndef RMD_OTF_SWEEP
-#define RMD_OTF_SWEEP 0
-#endif
 // ablation for A/B timing only (wrong results): 1 = no output stores, 2 = no MFMA tasks, 3 = tasks
 // without MFMAs (operand loads and puts), 4 = tasks without operand loads (MFMAs on one task's operands)
 #ifndef RMD_OTF_ABL
@@ -584,244 +580,6 @@ otf_lookup_kernel(const T* __restrict__ qseg, const T* __restrict__ tseg, OtfGeo
             if (y >= g.H || x >= g.W) continue;
             const float fy = sfy[L][q] + (sfx[L][q] - sfx[L][q]);   // a NaN x weight reaches rows outside the band too
             if (RMD_OTF_ABL == 1 && fy != 12345.f) continue;
-            float* o = ob + (size_t)(a * D) * N + y * g.W + x;
-#pragma unroll
-            for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
-        }
-    }
-}
-
-// ---- row-sweep lookup (round 6) -------------------------------------------------------------------
-// C = 256 (bf16 or split-bf16 operands), r <= 4.  One 512-thread workgroup per (batch, 16 x 8 query
-// block); wave w owns query row w of the block (one 16-query segment), its query fragments in registers.
-// Per level the block's target box is swept one unit = (box row, <= kSwN segments) at a time: all eight
-// waves stage the unit in LDS (two LDS stages, the following unit's 16-B pieces in flight in registers
-// while the current one is computed), and each wave whose own window rows and segments meet the unit
-// runs its 16 x 16 tiles on it (A = target fragments from LDS, B = its query fragments) and keeps the
-// products inside each query's (2r+2)^2 patch, as otf_lookup_kernel does.  Every target segment of the
-// box crosses L2 -> CU once per 128 queries instead of once per 32 (the 16 x 2 blocks of
-// otf_lookup_kernel each load their own box; profiles/otf_pmc_r05.json: ~0.9 GB of such loads per cfg2
-// lookup), and the MFMA A operands come from LDS instead of L2.
-constexpr int kSwQY = 8, kSwThreads = 512, kSwQ = 16 * kSwQY;
-template <int NP> struct Sw {
-    static constexpr int NSW = 4 / NP;                // segments per unit
-    static constexpr int SEGB = 16 * 256 * 2 * NP;    // bytes per target segment at C = 256
-    static constexpr int UNITB = NSW * SEGB;          // 32 KiB
-    static constexpr int PIECES = UNITB / (kSwThreads * 16);
-};
-template <int R> constexpr size_t sweep_lds_bytes() {
-    return (size_t)(kSwQ * otf_patch_stride(R) * 4 + 15) / 16 * 16 + 2 * (size_t)Sw<1>::UNITB +
-           4 * RMD_MAX_LEVELS * kSwQ * 4 + RMD_MAX_LEVELS * 4 * 4;
-}
-
-template <bool X3, int R>
-__global__ void __launch_bounds__(kSwThreads, 1)
-otf_sweep_kernel(const __bf16* __restrict__ qseg, const __bf16* __restrict__ tseg, OtfGeom g,
-                 const float* __restrict__ coords, unsigned zmask, float* __restrict__ out) {
-    using SW = Sw<X3 ? 2 : 1>;
-    using SG = Seg<__bf16>;
-    constexpr int NP = X3 ? 2 : 1, NLS = 8 * NP;
-    constexpr int D = 2 * R + 1, K = 2 * R + 2, KK = K * K, KKp = otf_patch_stride(R);
-    constexpr int ITEMS = (kSwQ * D + kSwThreads - 1) / kSwThreads;
-    constexpr size_t segsz = (size_t)16 * 256 * NP;  // elements per segment
-    extern __shared__ __attribute__((aligned(16))) unsigned char sw_lds[];
-    float* S = reinterpret_cast<float*>(sw_lds);                                      // [kSwQ][KKp]
-    unsigned char* stg = sw_lds + (kSwQ * KKp * 4 + 15) / 16 * 16;                     // 2 x UNITB
-    int* sxs = reinterpret_cast<int*>(stg + 2 * SW::UNITB);                            // [L][kSwQ]
-    int* sys = sxs + RMD_MAX_LEVELS * kSwQ;
-    float* sfx = reinterpret_cast<float*>(sys + RMD_MAX_LEVELS * kSwQ);
-    float* sfy = sfx + RMD_MAX_LEVELS * kSwQ;
-    int* box = reinterpret_cast<int*>(sfy + RMD_MAX_LEVELS * kSwQ);                   // [L][4]
-    const int nbx = (g.W + 15) >> 4, nqb = nbx * ((g.H + kSwQY - 1) / kSwQY);
-    const int lid = xcd_block(blockIdx.x, gridDim.x);
-    const int qb = lid % nqb, b = lid / nqb;
-    const int qx0 = (qb % nbx) * 16, qy0 = (qb / nbx) * kSwQY;
-    const int N = g.H * g.W;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n = lane & 15, gq = lane >> 4;
-
-    // this wave's query row: fragments of its segment, all load steps (hi / lo interleaved for X3)
-    const int qrow = min(qy0 + w, g.H - 1);
-    const __bf16* qsb = qseg + ((size_t)b * g.QS + (size_t)qrow * g.qnsx + (qx0 >> 4)) * segsz;
-    bf16x8 qf[NLS];
-#pragma unroll
-    for (int ls = 0; ls < NLS; ++ls) qf[ls] = *reinterpret_cast<const bf16x8*>(qsb + ((size_t)ls * 64 + lane) * 8);
-
-    // windows: lane (n, level gq) of wave w = query w*16 + n at level gq (coords clamped as rmd_corr_lookup)
-    if (tid < RMD_MAX_LEVELS * 4) box[tid] = (tid & 1) ? -(1 << 30) : (1 << 30);
-    __syncthreads();
-    int mnx = 1 << 30, mxx = -(1 << 30), mny = 1 << 30, mxy = -(1 << 30);
-    if (gq < g.L) {
-        const int q = w * 16 + n;
-        const int x = min(qx0 + n, g.W - 1);
-        const float cx0 = coords[((size_t)b * 2 + 0) * N + qrow * g.W + x];
-        const float cy0 = coords[((size_t)b * 2 + 1) * N + qrow * g.W + x];
-        const float inv = 1.0f / (float)(1 << gq);
-        const float rx = cx0 * inv, ry = cy0 * inv;
-        const float cx = fminf(fmaxf(rx, -1.0e6f), 1.0e6f);
-        const float cy = fminf(fmaxf(ry, -1.0e6f), 1.0e6f);
-        const int xs = (int)floorf(cx) - R, ys = (int)floorf(cy) - R;
-        sxs[gq * kSwQ + q] = xs;
-        sys[gq * kSwQ + q] = ys;
-        sfx[gq * kSwQ + q] = rx - floorf(rx);           // NaN / inf coordinate -> NaN window (grid_sample)
-        sfy[gq * kSwQ + q] = ry - floorf(ry);
-        mnx = xs; mxx = xs + K - 1; mny = ys; mxy = ys + K - 1;
-    }
-    // the wave's window union per level (16-lane groups), then the block's box
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        mnx = min(mnx, __shfl_xor(mnx, o));
-        mxx = max(mxx, __shfl_xor(mxx, o));
-        mny = min(mny, __shfl_xor(mny, o));
-        mxy = max(mxy, __shfl_xor(mxy, o));
-    }
-    if (gq < g.L && n == 0) {
-        atomicMin(&box[gq * 4 + 0], mnx);
-        atomicMax(&box[gq * 4 + 1], mxx);
-        atomicMin(&box[gq * 4 + 2], mny);
-        atomicMax(&box[gq * 4 + 3], mxy);
-    }
-    __syncthreads();                                    // windows and boxes complete
-
-    for (int L = 0; L < g.L; ++L) {
-        const int lh = g.lh[L], lw = g.lw[L];
-        float* ob = out + ((size_t)b * g.L + L) * D * D * (size_t)N;
-        const bool masked = (zmask >> L) & 1u;
-        if (masked || lh < 2 || lw < 2) {               // raft_fs.py:77-78; 1-pixel levels divide by zero
-            const float v = masked ? 0.f : __builtin_nanf("");
-            for (int idx = tid; idx < kSwQ * D * D; idx += kSwThreads) {
-                const int q = idx % kSwQ, c = idx / kSwQ;
-                const int y = qy0 + q / 16, x = qx0 + q % 16;
-                if (y < g.H && x < g.W) ob[(size_t)c * N + y * g.W + x] = v;
-            }
-            continue;
-        }
-        const int bx0 = max(box[L * 4 + 0], 0), bx1 = min(box[L * 4 + 1], lw - 1);
-        const int by0 = max(box[L * 4 + 2], 0), by1 = min(box[L * 4 + 3], lh - 1);
-        const int rows = max(by1 - by0 + 1, 0);
-        const int sa = bx0 >> 4, nseg = bx1 >= bx0 ? (bx1 >> 4) - sa + 1 : 0;
-        const int nch = (nseg + SW::NSW - 1) / SW::NSW;
-        const int U = rows * nch;
-        const __bf16* tlev = tseg + ((size_t)b * g.TS + g.soff[L]) * segsz;
-
-        float hx[ITEMS][K];
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-#pragma unroll
-            for (int jj = 0; jj < K; ++jj) hx[i][jj] = 0.f;
-
-        if (U > 0 && rows * nseg <= kMaxTasks) {
-            for (int i = tid; i < kSwQ * KKp; i += kSwThreads) S[i] = 0.f;
-            // this wave's window rows / segments at level L (uniform), clipped to the box
-            const int wy0 = max(__builtin_amdgcn_readlane(mny, 16 * L), by0);
-            const int wy1 = min(__builtin_amdgcn_readlane(mxy, 16 * L), by1);
-            const int ws0 = max(__builtin_amdgcn_readlane(mnx, 16 * L), bx0) >> 4;
-            const int ws1 = min(__builtin_amdgcn_readlane(mxx, 16 * L), bx1) >> 4;
-            const int q = w * 16 + n;                   // this lane's query (MFMA column n)
-            const int qys = sys[L * kSwQ + q], qxs = sxs[L * kSwQ + q];
-            float* P = S + q * KKp;
-            uint4 pr[SW::PIECES];
-            auto load = [&](int u) {
-                const int rr = u / nch, c0 = sa + (u - rr * nch) * SW::NSW;
-                const unsigned char* src = reinterpret_cast<const unsigned char*>(
-                    tlev + ((size_t)(by0 + rr) * g.nsx[L] + c0) * segsz);
-                const int nv = min(SW::NSW, sa + nseg - c0);          // segments of the unit inside the box
-#pragma unroll
-                for (int i = 0; i < SW::PIECES; ++i) {
-                    const int off = (i * kSwThreads + tid) * 16;
-                    if (off < nv * SW::SEGB) pr[i] = *reinterpret_cast<const uint4*>(src + off);
-                }
-            };
-            auto write = [&](int s) {
-#pragma unroll
-                for (int i = 0; i < SW::PIECES; ++i)
-                    *reinterpret_cast<uint4*>(stg + s * SW::UNITB + (i * kSwThreads + tid) * 16) = pr[i];
-            };
-            load(0);
-            write(0);
-            if (U > 1) load(1);
-            __syncthreads();                            // stage 0 and the zeroed patches visible
-            for (int u = 0; u < U; ++u) {
-                const int rr = u / nch, r = by0 + rr, c0 = sa + (u - rr * nch) * SW::NSW;
-                if (r >= wy0 && r <= wy1) {
-                    const int j0 = max(ws0, c0) - c0, j1 = min(ws1, c0 + SW::NSW - 1) - c0;
-                    const unsigned char* ab = stg + (u & 1) * SW::UNITB + lane * 16;
-                    for (int j = j0; j <= j1; ++j) {
-                        f32x4 acc = {};
-#pragma unroll
-                        for (int ks = 0; ks < 8; ++ks) {
-                            if constexpr (X3) {
-                                const bf16x8 th = *reinterpret_cast<const bf16x8*>(ab + j * SW::SEGB + (2 * ks) * 1024);
-                                const bf16x8 tl = *reinterpret_cast<const bf16x8*>(ab + j * SW::SEGB + (2 * ks + 1) * 1024);
-                                SG::mma(acc, tl, qf[2 * ks]);            // lo.hi, hi.lo first, hi.hi last
-                                SG::mma(acc, th, qf[2 * ks + 1]);
-                                SG::mma(acc, th, qf[2 * ks]);
-                            } else {
-                                SG::mma(acc, *reinterpret_cast<const bf16x8*>(ab + j * SW::SEGB + ks * 1024), qf[ks]);
-                            }
-                        }
-                        // C[target 4 gq + e][query n] of segment c0 + j: keep the products inside the
-                        // query's patch, the others to its never-read pad slot (no branches)
-                        const int dy = r - qys, dx0 = (c0 + j) * 16 + 4 * gq - qxs;
-                        const bool rok = (unsigned)dy < (unsigned)K;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) P[rok && (unsigned)(dx0 + e) < (unsigned)K ? dy * K + dx0 + e : KK] = acc[e];
-                    }
-                }
-                if (u + 1 < U) write((u + 1) & 1);
-                __syncthreads();
-                if (u + 2 < U) load(u + 2);
-            }
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const int idx = tid + i * kSwThreads;
-                if (idx >= kSwQ * D) break;
-                const int qq = idx % kSwQ, a = idx / kSwQ;
-                const float fx = sfx[L * kSwQ + qq];
-                const float* Pq = S + qq * KKp + a;
-#pragma unroll
-                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Pq[jj * K + 1] - Pq[jj * K], Pq[jj * K]);
-            }
-            __syncthreads();                            // S is free for the next level
-        } else if (U > 0) {
-            // a box of more than kMaxTasks (row, segment) pairs: each query's own (2r+2)^2 patch, one
-            // dot product per thread (as otf_lookup_kernel)
-            for (int idx = tid; idx < kSwQ * KK; idx += kSwThreads) {
-                const int q = idx / KK, r = idx - q * KK;
-                const int ty = sys[L * kSwQ + q] + r / K, tx = sxs[L * kSwQ + q] + r % K;
-                float acc = 0.f;
-                if (ty >= 0 && ty < lh && tx >= 0 && tx < lw) {
-                    const __bf16* qs = qseg + ((size_t)b * g.QS + (size_t)min(qy0 + q / 16, g.H - 1) * g.qnsx + (qx0 >> 4)) * segsz;
-                    const __bf16* ts = tlev + ((size_t)ty * g.nsx[L] + (tx >> 4)) * segsz;
-                    for (int c = 0; c < g.C; ++c)
-                        acc = fmaf(seg_elem<__bf16, X3>(qs, q % 16, c), seg_elem<__bf16, X3>(ts, tx & 15, c), acc);
-                }
-                S[q * KKp + r] = acc;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const int idx = tid + i * kSwThreads;
-                if (idx >= kSwQ * D) break;
-                const int qq = idx % kSwQ, a = idx / kSwQ;
-                const float fx = sfx[L * kSwQ + qq];
-                const float* Pq = S + qq * KKp + a;
-#pragma unroll
-                for (int jj = 0; jj < K; ++jj) hx[i][jj] = fmaf(fx, Pq[jj * K + 1] - Pq[jj * K], Pq[jj * K]);
-            }
-            __syncthreads();
-        }
-
-        // y-interpolation and the (a, b)-major output planes
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            const int idx = tid + i * kSwThreads;
-            if (idx >= kSwQ * D) break;
-            const int qq = idx % kSwQ, a = idx / kSwQ;
-            const int y = qy0 + qq / 16, x = qx0 + qq % 16;
-            if (y >= g.H || x >= g.W) continue;
-            const float fy = sfy[L * kSwQ + qq] + (sfx[L * kSwQ + qq] - sfx[L * kSwQ + qq]);
             float* o = ob + (size_t)(a * D) * N + y * g.W + x;
 #pragma unroll
             for (int bb = 0; bb < D; ++bb) o[(size_t)bb * N] = fmaf(fy, hx[i][bb + 1] - hx[i][bb], hx[i][bb]);
@@ -1533,36 +1291,6 @@ extern "C" int rmd_corr_otf_lookup(const void* workspace, int batch, int channel
         case 6: RMD_OTF_C(T, 6, QX, QY, OC); break;                  \
         case 7: RMD_OTF_C(T, 7, QX, QY, OC); break;                  \
         default: RMD_OTF_C(T, 8, QX, QY, OC); break;                 \
-    }
-    // C = 256, r <= 4, bf16 / split-bf16: the row-sweep kernel (otf_sweep_kernel)
-    if (RMD_OTF_SWEEP && g.Cp == 256 && radius <= 4 && (compute == RMD_BF16 || x3)) {
-        const long long nblk = (long long)((width + 15) / 16) * ((height + kSwQY - 1) / kSwQY) * batch;
-        RMD_REQUIRE(nblk < (1ll << 31), RMD_ERR_SHAPE, "rmd_corr_otf_lookup: grid too large");
-        const __bf16* q = reinterpret_cast<const __bf16*>(workspace);
-        const size_t tq = qn * (x3 ? 2 : 1);
-#define RMD_SW(XX, RR)                                                                                       \
-    do {                                                                                                     \
-        auto k = otf_sweep_kernel<XX, RR>;                                                                   \
-        const size_t lds = sweep_lds_bytes<RR>();                                                            \
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                  (int)lds);                                                                 \
-        k<<<(unsigned)nblk, kSwThreads, lds, st>>>(q, q + tq, g, coords, zero_level_mask, out);               \
-    } while (0)
-#define RMD_SW_R(XX)                          \
-    switch (radius) {                         \
-        case 1: RMD_SW(XX, 1); break;         \
-        case 2: RMD_SW(XX, 2); break;         \
-        case 3: RMD_SW(XX, 3); break;         \
-        default: RMD_SW(XX, 4); break;        \
-    }
-        if (x3) {
-            RMD_SW_R(true)
-        } else {
-            RMD_SW_R(false)
-        }
-#undef RMD_SW_R
-#undef RMD_SW
-        return check_launch("rmd_corr_otf_lookup/sweep");
     }
     // bf16 on wide maps (at least kWideBlocks 16x2 query blocks): 16x4 blocks at 512 threads read 45 %
     // fewer target bytes per query; at the 4K map (b2, 270x480) 362 us vs 396 us per lookup, at cfg2
