@@ -874,6 +874,14 @@ def main():
         # rank 0 profiles its own GPU in child processes after the timed region (the other ranks go on
         # to the next leg and wait for rank 0 at its first barrier)
         live = rank == 0 and args.live_pmc == "on"
+        # both timed legs run before any profiling child process: the counter passes leave the chip in
+        # another power / thermal state for a while, and the power-bound x3 GEMM of the fp32 leg ran ~15 %
+        # slower right after them (profiles/INDEX_r06.md)
+        fp32_leg = args.fp32_mode == "on" and args.precision != "fp32"
+        if fp32_leg:
+            progress(rank, "fp32_mode leg")
+            w32 = max(3, args.warmup)
+            el32, eg32, el32l = corr_leg(args, "fp32", inputs, world, device, args.fp32_steps, w32)
         traffic, note = live_traffic(args, args.precision, B, rank, device) if live else (None, "")
         if traffic is None:
             fallback, fnote = stored_traffic(args.precision)
@@ -885,10 +893,8 @@ def main():
         res["roofline_gemm"] = roof_gemm
         res["roofline_lookup"] = roof_look
         progress(rank, "headline leg done")
-        if args.fp32_mode == "on" and args.precision != "fp32":
+        if fp32_leg:
             # the parity mode (north_star's fp32 gate) on the same inputs: x3 GEMM + 24-bit pyramid
-            progress(rank, "fp32_mode leg")
-            el32, eg32, el32l = corr_leg(args, "fp32", inputs, world, device, args.fp32_steps, 3)
             tr32, n32 = live_traffic(args, "fp32", B, rank, device) if live else (None, "")
             if tr32 is None:
                 fb, fn = stored_traffic("fp32")
@@ -898,7 +904,7 @@ def main():
             if rank == 0:
                 res["fp32_mode"] = {"value": world * B * args.fp32_steps / el32, "unit": "frame-pairs/s",
                                     "ms_per_step": el32 / args.fp32_steps * 1e3, "steps": args.fp32_steps,
-                                    "warmup": 3, "precision": "fp32", "dtype": "fp32",
+                                    "warmup": w32, "precision": "fp32", "dtype": "fp32",
                                     "pyramid_storage": STORAGE_NAME[storage_bytes("fp32")],
                                     "storage_note": ("'fp32' mode stores the pyramid as RMD_S24: each fp32 value "
                                                      "rounded to its top 24 bits (16 significant bits, <= 2^-16 "

@@ -8,13 +8,15 @@
 // runs as three v_mfma_f32_16x16x32_bf16 per k-step into one fp32 accumulator: 3/16 of the exact-
 // f32 MFMA cost.  The 1/sqrt(C) scale is folded into fmap2 before the split (fp32 multiply).
 //
-// Geometry: one workgroup (8 waves, two per SIMD, ping-pong phases) owns an 8 x 16
+// Geometry: one workgroup (8 waves, two per SIMD, free-running) owns an 8 x 16
 // block of target pixels — both split halves of its A operand sit in LDS as a k-major image — and
 // each wave sweeps its own 32-query tiles (8 M-tiles of 16 targets x 2 N-tiles of 16 queries x 8
 // k-steps x 3 products), then pools in-lane and stores all four levels straight from the
 // accumulators with range-checked buffer stores (rows past the level fall outside the descriptor,
-// chunks past the row get a 1 GiB bias), as fp32 or as RMD_S24 (3-byte) values.  The 32x32x16 form
-// of rounds 2-4 is in git history (commit db30b41 and before; profiles/x3_ab_r05.json compares them).
+// chunks past the row get a 1 GiB bias), as fp32 or as RMD_S24 (3-byte) values (epilogue16_s24, round
+// 6).  Partial last rounds of one-CU workgroups are balanced by splitting the remaining blocks' query
+// tiles (X3Sched).  The 32x32x16 form of rounds 2-4 is in git history (commit db30b41 and before;
+// profiles/x3_ab_r05.json compares them).
 
 #include "rmd_common.h"
 #include "corr_x3.h"
@@ -208,13 +210,21 @@ __device__ __forceinline__ void swap16(unsigned& x, unsigned& y) {
 #ifndef RMD_X3_ABL
 #define RMD_X3_ABL 0
 #endif
+// RMD_X3_FREE: 1 (product since round 6) = no ping-pong phase barriers, the two waves of a SIMD run
+// free; 0 = waves w and w + 4 alternate MFMA and epilogue phases between workgroup barriers.  With the
+// round-5 epilogue (~875 VALU per tile) the phases had to be separated; with epilogue16_s24 (~280) the
+// barriers cost more than they hide: cfg2 0.464-0.466 vs 0.477-0.479 ms in the bench step, GRBM cycles
+// 6.89M vs 7.42M, MFMA busy 0.69 vs 0.64 (profiles/x3_free_ab_r06.json)
+#ifndef RMD_X3_FREE
+#define RMD_X3_FREE 1
+#endif
 // RMD_X3_S24_R05 = 1: the round-5 S24 epilogue (epilogue16<true>) instead of epilogue16_s24 (A/B only)
 #ifndef RMD_X3_S24_R05
 #define RMD_X3_S24_R05 0
 #endif
 
 // ---- GEMM kernel (16x16x32 MFMA) ------------------------------------------------------------------
-// One workgroup (8 waves, two per SIMD, ping-pong phases) owns an 8 x 16 target block; its waves
+// One workgroup (8 waves, two per SIMD, free-running: RMD_X3_FREE) owns an 8 x 16 target block; its waves
 // sweep their own 32-query tiles through a B-fragment register ring, with v_mfma_f32_16x16x32_bf16 tiles:
 // a wave's 32-query tile is 2 N-tiles of 16 queries against 8 M-tiles of 16 targets (M-tile mt = 2 rp
 // + ch: rows 2rp, 2rp+1 x cols 8ch..8ch+7 of the block), 8 k-steps of 32 channels, each k-step in two
@@ -578,11 +588,12 @@ __device__ __forceinline__ void x3_segment(const __bf16* __restrict__ aHi, const
             }
     }
     vmcnt_pad_n<S24 ? (RMD_X3_S24_R05 ? kEpiStores16 + 1 : kEpiStoresS24) : kEpiStores16>(pyr);
-    // ping-pong phases as corr_pyramid_x3: waves w and w + 4 of each SIMD alternate MFMA and epilogue
+    // free-running waves (RMD_X3_FREE), or ping-pong phases: waves w and w + 4 of each SIMD alternate MFMA
+    // and epilogue
     const int nmax = (qhi - qlo + WAVES - 1) / WAVES;
     const int nw = qt < qhi ? (qhi - qt + WAVES - 1) / WAVES : 0;
     const bool late = w >= 4;
-    if (late && ABL < 3) __builtin_amdgcn_s_barrier();
+    if (late && ABL < 3 && !RMD_X3_FREE) __builtin_amdgcn_s_barrier();
     for (int k = 0; k < nmax; ++k) {
         const int qn = qt + WAVES;
         if (k < nw) {
@@ -591,7 +602,7 @@ __device__ __forceinline__ void x3_segment(const __bf16* __restrict__ aHi, const
             read_a16<0, 0>(a0, smem, bhi, blo);
             ksteps16<0>(acc, a0, a1, rh, rl, smem, bhi, blo, bq + (size_t)qt * 8192, bq + (size_t)min(qn, nqt - 1) * 8192,
                         lo_off);
-            if (ABL < 3) __builtin_amdgcn_s_barrier();
+            if (ABL < 3 && !RMD_X3_FREE) __builtin_amdgcn_s_barrier();
             if constexpr (ABL >= 2) {
 #pragma unroll
                 for (int mt = 0; mt < 8; ++mt) asm volatile("" ::"v"(acc[mt][0]), "v"(acc[mt][1]));
@@ -603,14 +614,14 @@ __device__ __forceinline__ void x3_segment(const __bf16* __restrict__ aHi, const
             } else {
                 epilogue16<S24>(acc, L, qt, N, n, gq);
             }
-            if (ABL < 3) __builtin_amdgcn_s_barrier();
-        } else if (ABL < 3) {
+            if (ABL < 3 && !RMD_X3_FREE) __builtin_amdgcn_s_barrier();
+        } else if (ABL < 3 && !RMD_X3_FREE) {
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_s_barrier();
         }
         qt = qn;
     }
-    if (!late && ABL < 3) __builtin_amdgcn_s_barrier();
+    if (!late && ABL < 3 && !RMD_X3_FREE) __builtin_amdgcn_s_barrier();
 }
 
 // Balanced schedule (round 6).  At cfg2 the 448 (image, block) workgroups of one-CU size run 1.75
