@@ -404,6 +404,34 @@ def test_w8_balanced_schedule_levels_vs_oracle(b, h, w):
         assert rel_max_err(got, r) < 1e-2, f"level {i}"
 
 
+@pytest.mark.parametrize("b,h,w", [(8, 48, 96), (8, 55, 128), (16, 55, 128), (8, 9, 70)])
+def test_x3_balanced_schedule_whole_pyramid_vs_exact(b, h, w):
+    """The fp32-mode GEMM's balanced schedule (corr_pyramid_x3.hip X3Sched): when one workgroup per
+    (image, block) leaves a partial last round, each XCD's remaining blocks run as query-tile parts
+    (8x48x96: 36 blocks per XCD -> 32 whole + 4 x 8 parts; cfg2 b8: 32 + 24 x 4; b16: 96 + 16 x 2;
+    8x9x70: 2 x 5 blocks per image, 80 units, one round, no split).  Every element of every level (a
+    missed or doubled query tile would show) against the exact-f32 GEMM's pyramid: max-normalised
+    1e-4 and north_star's elementwise gate (S24 storage, <= 2^-16 relative rounding)."""
+    import rmd
+    rng = np.random.default_rng(b * 1000 + h * w)
+    c = 256
+    f1 = _t(rng.standard_normal((b, c, h, w)).astype(np.float32))
+    f2 = _t(rng.standard_normal((b, c, h, w)).astype(np.float32))
+    p24 = rmd.ops.corr_pyramid(f1, f2, 4, "fp32")
+    p32 = rmd.ops.corr_pyramid(f1, f2, 4, "fp32-exact")
+    for i in range(4):
+        got = p24.unpack(i).reshape(-1).double()         # compared on the GPU (b16: 0.9 G elements)
+        ref = p32.unpack(i).reshape(-1).double()
+        assert torch.isfinite(ref).all() and torch.equal(torch.isnan(got), torch.isnan(ref))
+        scale = ref.abs().max()
+        err = (got - ref).abs()
+        assert float(err.max() / scale) < 1e-4, f"level {i}"
+        assert bool((err <= 1e-4 * ref.abs() + 1e-5 * scale).all()), f"level {i} elementwise"
+        del got, ref, err
+    del p24, p32
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("precision,c,b,h,w", [("bf16", 200, 2, 23, 40), ("bf16", 193, 1, 17, 33),
                                                ("fp32", 200, 2, 23, 40), ("fp32", 96, 3, 9, 70),
                                                ("fp32", 256, 1, 8, 8)])

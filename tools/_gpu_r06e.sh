@@ -2,7 +2,7 @@
 # kernel stats of the bench command (live PMC off under the tracer)
 set -o pipefail
 export TMPDIR=/tmp
-R=gpurun_out/r06e
+R=gpurun_out/${RUN:-r06e}
 mkdir -p $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || { tail -30 $R/tests.log; exit 2; }
 tail -2 $R/tests.log
