@@ -404,17 +404,18 @@ def test_w8_balanced_schedule_levels_vs_oracle(b, h, w):
         assert rel_max_err(got, r) < 1e-2, f"level {i}"
 
 
-@pytest.mark.parametrize("b,h,w", [(8, 48, 96), (8, 55, 128), (16, 55, 128), (8, 9, 70)])
-def test_x3_balanced_schedule_whole_pyramid_vs_exact(b, h, w):
+@pytest.mark.parametrize("b,h,w,c", [(8, 48, 96, 256), (8, 55, 128, 256), (16, 55, 128, 256), (8, 9, 70, 256),
+                                     (8, 39, 121, 256), (8, 39, 121, 96)])
+def test_x3_balanced_schedule_whole_pyramid_vs_exact(b, h, w, c):
     """The fp32-mode GEMM's balanced schedule (corr_pyramid_x3.hip X3Sched): when one workgroup per
     (image, block) leaves a partial last round, each XCD's remaining blocks run as query-tile parts
     (8x48x96: 36 blocks per XCD -> 32 whole + 4 x 8 parts; cfg2 b8: 32 + 24 x 4; b16: 96 + 16 x 2;
-    8x9x70: 2 x 5 blocks per image, 80 units, one round, no split).  Every element of every level (a
-    missed or doubled query tile would show) against the exact-f32 GEMM's pyramid: max-normalised
-    1e-4 and north_star's elementwise gate (S24 storage, <= 2^-16 relative rounding)."""
+    8x9x70: 2 x 5 blocks per image, 80 units, one round, no split; 8x39x121: 40 blocks per XCD -> 32 + 8 x 4
+    parts with a partial last query tile (N = 4719) and ragged columns, also at C = 96).  Every element of
+    every level (a missed or doubled query tile would show) against the exact-f32 GEMM's pyramid:
+    max-normalised 1e-4 and north_star's elementwise gate (S24 storage, <= 2^-16 relative rounding)."""
     import rmd
-    rng = np.random.default_rng(b * 1000 + h * w)
-    c = 256
+    rng = np.random.default_rng(b * 1000 + h * w + c)
     f1 = _t(rng.standard_normal((b, c, h, w)).astype(np.float32))
     f2 = _t(rng.standard_normal((b, c, h, w)).astype(np.float32))
     p24 = rmd.ops.corr_pyramid(f1, f2, 4, "fp32")
