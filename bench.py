@@ -436,6 +436,7 @@ def dicl_leg(args, world, rank, device):
     disp = torch.stack(torch.meshgrid(torch.arange(-md[0], md[0] + 1.0), torch.arange(-md[1], md[1] + 1.0),
                                       indexing="ij")).view(1, 2, du, dv, 1, 1).to(device)
     vol_bytes = 0
+    stack_args = {}
 
     def forward():
         nonlocal vol_bytes
@@ -446,9 +447,11 @@ def dicl_leg(args, world, rank, device):
             mnet, dap = mods[l]
             if flow is None:
                 mvol = ops.dicl_stack_int(f1, f2, md[0], md[1])
+                stack_args[l] = None
             else:
                 up = 2.0 * F.interpolate(flow, (h, w), mode="bilinear", align_corners=True)
                 mvol = ops.dicl_stack_int_warped(f1, f2, up, md[0], md[1])
+                stack_args[l] = up
             vb += mvol.numel() * 4
             cost = dap(mnet(mvol))
             prob = F.softmax(cost.reshape(b, du * dv, h, w), dim=1).view(b, 1, du, dv, h, w)
@@ -470,16 +473,38 @@ def dicl_leg(args, world, rank, device):
             out = forward()
         torch.cuda.synchronize(device)
         el = time.perf_counter() - t0
+        # the five volume launches alone, on the inputs of the last forward (HIP events on the stream
+        # the C ABI launches on): algorithmic bytes = the fp32 volumes written + both feature maps (and
+        # the upsampled flow) read once
+        vreps = 20
+        a = torch.cuda.Event(enable_timing=True)
+        z = torch.cuda.Event(enable_timing=True)
+        io_bytes = vol_bytes
+        for l in levels:
+            io_bytes += 2 * feats[l][0].numel() * 4 + (stack_args[l].numel() * 4 if stack_args[l] is not None else 0)
+        a.record()
+        for _ in range(vreps):
+            for l in levels:
+                f1, f2 = feats[l]
+                if stack_args[l] is None:
+                    ops.dicl_stack_int(f1, f2, md[0], md[1])
+                else:
+                    ops.dicl_stack_int_warped(f1, f2, stack_args[l], md[0], md[1])
+        z.record()
+        torch.cuda.synchronize(device)
+        vol_ms = a.elapsed_time(z) / vreps
     if world > 1:
         torch.distributed.barrier()
     el = job_time(el, world, device)
     fin = bool(torch.isfinite(out).all())
-    del mods, feats, out
+    del mods, feats, out, stack_args
     torch.cuda.empty_cache()
     return {"workload": "DICL cost volumes + MatchingNet + DAP + soft-argmin, coarse to fine (levels 6..2) at "
                         "384x512 (BASELINE configs[2], SURVEY cfg3)",
             "frame_pairs_per_s": world * b * reps / el, "ms_per_batch": el / reps * 1e3, "per_gpu_batch": b,
             "global_batch": world * b, "n_gpus": world, "volume_bytes_per_batch": vol_bytes,
+            "volume_ms_per_batch": vol_ms, "volume_io_bytes_per_batch": io_bytes,
+            "volume_gbps": io_bytes / vol_ms / 1e6, "volume_frac_of_hbm_peak": io_bytes / vol_ms / 1e6 / 8000.0,
             "displacement_range": list(md), "channels": c, "finite": fin,
             "scaling": "strong" if args.global_batch else "weak", "dtype": "fp32",
             "data": "synthetic feature maps (encoder / context nets outside the hot path)"}
