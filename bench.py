@@ -410,6 +410,16 @@ def hybrid_leg(args, world, rank, device):
             "data": "synthetic smooth pairs (tests/golden/synth.py), name-keyed random weights"}
 
 
+def _library_info():
+    """The measured librmd.so: its path, version and source fingerprint, and whether that fingerprint
+    matches the sources in this tree (csrc/Makefile; rmd/_lib.py build_info)."""
+    from rmd import _lib
+    info = _lib.build_info()
+    info["path"] = os.path.relpath(_lib.LIB_PATH, ROOT)
+    info["version"] = _lib.lib().rmd_version().decode()
+    return info
+
+
 def dicl_leg(args, world, rank, device):
     """BASELINE configs[2] / SURVEY.md §8(d) cfg3: the DICL baseline's matching stage coarse to fine at
     384x512, per-GPU b8, C = 32, displacement range (3, 3) (D = 49) on levels 6..2 (6x8 .. 96x128):
@@ -884,6 +894,7 @@ def main():
         "vs_baseline": None,
         "dtype": compute_dt,
         "data": "synthetic (seeded random 1/8-res feature maps + smooth moving flow; no dataset)",
+        "library": _library_info(),
         "config": {"workload": "RAFT all-pairs correlation + 4-level pyramid + 12 radius-4 lookups "
                                "(BASELINE configs[1]); the whole network is the 'model_level' key",
                    "image": f"{args.height}x{args.width} padded {H}x{W}", "feature_map": f"{h8}x{w8}",

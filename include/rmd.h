@@ -449,6 +449,12 @@ const char* rmd_version(void);
 #define RMD_ABI_VERSION 2
 int rmd_abi_version(void);
 
+/* Fingerprint of the sources this library was built from (16 hex digits of the sha256 of
+ * raft-meets-dicl_amd/csrc/{*.cpp,*.h,*.hip} in name order followed by this header; the Makefile
+ * computes it).  Not part of the reference interface: it lets a binding or a test tell a library
+ * rebuilt from the tree it sits in from a stale one.  Additive, so the ABI revision stays 2. */
+const char* rmd_source_hash(void);
+
 #ifdef __cplusplus
 }
 #endif

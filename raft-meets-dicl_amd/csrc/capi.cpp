@@ -28,6 +28,15 @@ extern "C" const char* rmd_version(void) { return "rmd 0.2 gfx950 abi 2"; }
 
 extern "C" int rmd_abi_version(void) { return RMD_ABI_VERSION; }
 
+// the Makefile's source fingerprint; the tagged string also lets rmd/_lib.py read it from the file
+// without loading the library
+#ifndef RMD_SRC_HASH
+#define RMD_SRC_HASH "unknown"
+#endif
+static const char kSrcTag[] = "rmd-src-hash:" RMD_SRC_HASH;
+
+extern "C" const char* rmd_source_hash(void) { return kSrcTag + 13; }
+
 extern "C" int rmd_pyramid_describe_layout(int batch, int height, int width, int levels, int storage, int layout,
                                            rmd_pyramid_desc* d) {
     if (!d) {

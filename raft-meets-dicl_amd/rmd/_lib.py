@@ -6,6 +6,7 @@ missing, or a tensor is not on the GPU, the call raises.
 """
 
 import ctypes
+import hashlib
 import os
 
 import torch  # noqa: F401  (load torch's libamdhip64 first so librmd.so binds to the same HIP runtime)
@@ -96,6 +97,7 @@ _SIGS = {
     "rmd_last_error": (ctypes.c_char_p, []),
     "rmd_version": (ctypes.c_char_p, []),
     "rmd_abi_version": (_I, []),
+    "rmd_source_hash": (ctypes.c_char_p, []),
 }
 
 # include/rmd.h RMD_ABI_VERSION this binding's signatures (_SIGS) were written for
@@ -119,6 +121,42 @@ def lib():
                            f"ABI {ABI_VERSION} (include/rmd.h RMD_ABI_VERSION); rebuild the library")
         _lib = l
     return _lib
+
+
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+_HEADER = os.path.join(os.path.dirname(os.path.dirname(_CSRC)), "include", "rmd.h")
+_SRC_TAG = b"rmd-src-hash:"
+
+
+def source_hash():
+    """The csrc/Makefile fingerprint recomputed from the tree (None without the sources): sha256 of
+    csrc/{*.cpp,*.h,*.hip} in name order, then include/rmd.h, first 16 hex digits."""
+    if not os.path.isdir(_CSRC) or not os.path.exists(_HEADER):
+        return None
+    names = sorted(n for n in os.listdir(_CSRC) if n.endswith((".cpp", ".h", ".hip")))
+    h = hashlib.sha256()
+    for p in [os.path.join(_CSRC, n) for n in names] + [_HEADER]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def library_source_hash(path=LIB_PATH):
+    """The fingerprint baked into a built library, read from the file without loading it."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    i = data.find(_SRC_TAG)
+    if i < 0:
+        return None
+    return data[i + len(_SRC_TAG):i + len(_SRC_TAG) + 16].decode("ascii", errors="replace")
+
+
+def build_info():
+    """{"source_hash": library's, "tree_hash": the sources', "sources_match": bool or None}."""
+    lh, th = library_source_hash(), source_hash()
+    return {"source_hash": lh, "tree_hash": th, "sources_match": (lh == th) if (lh and th) else None}
 
 
 def symbols():

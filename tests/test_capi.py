@@ -41,6 +41,19 @@ def test_abi_version_matches_header_and_binding():
     assert _lib.lib().rmd_version().endswith(b"abi 2")
 
 
+def test_library_was_built_from_these_sources():
+    """VERDICT r05 hygiene: the prebuilt library travels with the tree, so it must be the one these
+    sources build.  The Makefile bakes a fingerprint of csrc/ + include/rmd.h into it; the file's,
+    the loaded library's and the tree's fingerprints agree (build() rebuilds on a mismatch)."""
+    from rmd import _lib
+    info = _lib.build_info()
+    assert info["tree_hash"] is not None and len(info["tree_hash"]) == 16
+    assert info["source_hash"] == info["tree_hash"], (
+        f"librmd.so was built from other sources ({info['source_hash']} vs tree {info['tree_hash']}): "
+        f"run __graft_entry__.build()")
+    assert _lib.lib().rmd_source_hash().decode() == info["tree_hash"]
+
+
 def test_describe_cfg2_geometry():
     from rmd import _lib
     d = _lib.describe(8, 55, 128, 4, _lib.RMD_F16)
