@@ -120,6 +120,11 @@ constexpr unsigned kOOB = 0x80000000u;
 #if RMD_LOOKUP_ABL & 4
 __device__ unsigned g_abl_off = 0x80000000u;
 #endif
+// A/B knob: cache-policy bits of the pyramid loads (gfx950 CPol: 1 sc0, 2 nt, 16 sc1); 0 in the product
+#ifndef RMD_LOOKUP_LAUX
+#define RMD_LOOKUP_LAUX 0
+#endif
+constexpr int kLoadAux = RMD_LOOKUP_LAUX;
 
 // RMD_S24 storage element (include/rmd.h): bytes 1..3 of an fp32 word, little endian
 struct s24_t {
@@ -151,19 +156,19 @@ __device__ __forceinline__ void buf_words(unsigned (&dst)[NW], __amdgpu_buffer_r
     off |= g_abl_off;                 // ABL builds: every load to kOOB through a mutable global (not foldable)
 #endif
     if constexpr (NW == 4) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, kLoadAux);
 #pragma unroll
         for (int i = 0; i < 4; ++i) dst[i] = (unsigned)v[i];
     } else if constexpr (NW == 2) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, kLoadAux);
         dst[0] = (unsigned)v[0];
         dst[1] = (unsigned)v[1];
     } else if constexpr (NW == 1) {
-        dst[0] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+        dst[0] = (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, kLoadAux);
     } else {
 #pragma unroll
         for (int k = 0; k < NW / 4; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * k), 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(off + 16u * k), 0, kLoadAux);
 #pragma unroll
             for (int i = 0; i < 4; ++i) dst[4 * k + i] = (unsigned)v[i];
         }
@@ -182,7 +187,7 @@ __device__ __forceinline__ void buf_s24(unsigned (&dst)[CW], __amdgpu_buffer_rsr
         unsigned w[3 * CW / 4];
 #pragma unroll
         for (int k = 0; k < CW / 4; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(off + 12u * k), 0, kLoadAux);
             w[3 * k] = (unsigned)v[0];
             w[3 * k + 1] = (unsigned)v[1];
             w[3 * k + 2] = (unsigned)v[2];
