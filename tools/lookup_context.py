@@ -9,6 +9,9 @@ speed of the second.  Modes, each `steps` steps separated by a 50 ms idle gap ma
   nogemm   : the same 12 lookups per step on one pyramid built once (no GEMM between steps)
   oneout   : bench step with every lookup writing one preallocated output (C ABI call)
   samecoord: bench step with coords[0] for all 12 lookups
+  rev      : bench step with the coords in reverse order (coords[11] first)
+  shift    : bench step with coords[0] + 0.02 px * position (new tensors, nearly the same lines)
+  const11  : bench step with coords[11] for all 12 lookups
 usage: python3 tools/lookup_context.py [steps]"""
 import ctypes
 import json
@@ -37,7 +40,16 @@ def run(steps):
             if mode != "nogemm":
                 pyr = ops.corr_pyramid(f1, f2, 4, "bf16")
             for it in range(12):
-                co = coords[0] if mode == "samecoord" else coords[it]
+                if mode == "samecoord":
+                    co = coords[0]
+                elif mode == "rev":
+                    co = coords[11 - it]
+                elif mode == "shift":
+                    co = coords[0] + 0.02 * it
+                elif mode == "const11":
+                    co = coords[11]
+                else:
+                    co = coords[it]
                 if mode == "oneout":
                     _lib.check(lib.rmd_corr_lookup(ctypes.c_void_p(pyr.data.data_ptr()), ctypes.byref(pyr.desc),
                                                    ctypes.c_void_p(co.data_ptr()), 4, 0,
