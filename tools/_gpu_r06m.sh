@@ -3,7 +3,7 @@
 # x3 SQ counters (MFMA busy, clock) of the product
 set -o pipefail
 export TMPDIR=/tmp
-R=gpurun_out/r06m
+R=gpurun_out/${RUN:-r06m}
 mkdir -p $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/tests.log 2>&1 || { tail -30 $R/tests.log; exit 2; }
 tail -2 $R/tests.log
